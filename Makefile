@@ -1,0 +1,44 @@
+# Build libchunkio_amd.so (HIP kernels for gfx950 + C ABI) and the oracle.
+# `python -c "import __graft_entry__ as g; g.build()"` drives this file.
+
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+OUT     := chunkio_amd/lib
+LIB     := $(OUT)/libchunkio_amd.so
+SRC     := chunkio_amd/csrc
+BLD     := build
+INC     := -Iinclude -I$(SRC)
+
+CFLAGS   := -O3 -fPIC -Wall -Wextra -std=gnu11 $(INC)
+HIPFLAGS := -O3 -fPIC --offload-arch=$(ARCH) -std=c++17 -Wall $(INC) -munsafe-fp-atomics
+
+COBJS   := $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o
+HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/sha1_gpu.o
+
+all: $(LIB) oracle
+
+$(BLD)/%.o: $(SRC)/%.c $(wildcard $(SRC)/*.h) $(wildcard include/*/*.h)
+	@mkdir -p $(BLD)
+	$(CC) $(CFLAGS) -c -o $@ $<
+
+$(BLD)/%.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) $(wildcard include/*/*.h)
+	@mkdir -p $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(COBJS) $(HOBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: $(SRC)/crc32_gpu.hip
+	@mkdir -p $(BLD)/asm
+	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(BLD)/asm/crc32_gpu.s $<
+
+clean:
+	rm -rf $(BLD) $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle asm clean

@@ -1,0 +1,84 @@
+"""ctypes binding of libchunkio_amd.so (the C ABI in include/chunkio_amd/*.h).
+
+The shared library is built in-tree by `make` (or __graft_entry__.build()) into
+chunkio_amd/lib/.  There is no fallback: if the library is missing, importing
+any GPU entry point raises ImportError.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libchunkio_amd.so")
+
+# Every symbol the public headers declare (checked by tests/test_abi.py).
+EXPORTS = (
+    # include/crc32/crc32.h
+    "crc_update",
+    # include/chunkio_amd/cio_crc32_gpu.h
+    "cio_gpu_init", "cio_gpu_last_error", "cio_gpu_version",
+    "cio_crc32_shift", "cio_crc32_combine",
+    "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
+    "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_batch_dev", "cio_crc32_batch_host",
+    "cio_gpu_fill_synthetic", "cio_sha1_batch_dev",
+    "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
+    "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
+)
+
+_lib = None
+
+c_u64_p = ctypes.POINTER(ctypes.c_uint64)
+c_u32_p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _bind(lib):
+    V, P = ctypes.c_void_p, ctypes.POINTER
+    sig = {
+        "crc_update": (ctypes.c_uint64, [ctypes.c_uint64, V, ctypes.c_size_t]),
+        "cio_gpu_init": (ctypes.c_int, []),
+        "cio_gpu_last_error": (ctypes.c_char_p, []),
+        "cio_gpu_version": (ctypes.c_char_p, []),
+        "cio_crc32_shift": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
+        "cio_crc32_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+        "cio_crc32_plan_create": (ctypes.c_int, [P(V), c_u64_p, c_u64_p, ctypes.c_size_t]),
+        "cio_crc32_plan_destroy": (None, [V]),
+        "cio_crc32_plan_exec": (ctypes.c_int, [V, V, V, V, V]),
+        "cio_crc32_plan_exec_events": (ctypes.c_int, [V, V, V, V, V, V, V]),
+        "cio_crc32_plan_bytes": (ctypes.c_uint64, [V]),
+        "cio_crc32_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, V, ctypes.c_size_t, V]),
+        "cio_crc32_batch_host": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p,
+                                                ctypes.c_size_t]),
+        "cio_gpu_fill_synthetic": (ctypes.c_int, [V, c_u64_p, c_u64_p, c_u64_p, ctypes.c_size_t,
+                                                  ctypes.c_uint64, V]),
+        "cio_sha1_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, ctypes.c_size_t, V]),
+        "cio_gpu_event_create": (V, []),
+        "cio_gpu_event_destroy": (None, [V]),
+        "cio_gpu_event_record": (ctypes.c_int, [V, V]),
+        "cio_gpu_event_elapsed_ms": (ctypes.c_float, [V, V]),
+        "cio_gpu_stream_sync": (ctypes.c_int, [V]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib():
+    """Load (once) and return the bound library; raise ImportError if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is not built: run `make` or __graft_entry__.build()")
+        _lib = _bind(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+class CioGpuError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().cio_gpu_last_error()
+        raise CioGpuError(f"{what} failed: {msg.decode() if msg else 'unknown error'}")

@@ -1,0 +1,196 @@
+"""Host-side mirror of chunkio's CRC-32 interface over libchunkio_amd.so.
+
+Names and meaning follow the reference (fluent/chunkio):
+
+  crc_init() / crc_update(crc, data) / crc_finalize(crc)
+      deps/crc32/crc32.h:74-100, deps/crc32/crc32.c:337-390 -- raw state in
+      and out; crc_update on host bytes runs the library's scalar CPU path
+      (the drop-in `crc_update` symbol).
+  Crc32Plan / crc32_batch_dev()
+      the batched GPU path: N x cio_file_calculate_checksum()
+      (src/cio_file.c:66-94) over device-resident chunk contents.
+  crc32_shift() / crc32_combine()
+      GF(2) helpers to fold GPU partial CRCs into a running crc_cur
+      (src/cio_file.c:97-113).
+
+torch is used only as the device-memory container (tensors on cuda:N); every
+CRC computation goes through the C ABI.  There is no CPU fallback for the
+batched entry points: without the HIP library they raise.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+CRC_INIT = 0xFFFFFFFF
+
+
+def crc_init():
+    return CRC_INIT
+
+
+def crc_finalize(crc):
+    return (crc ^ 0xFFFFFFFF) & 0xFFFFFFFF
+
+
+def _as_bytes(data):
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8)
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
+def crc_update(crc, data):
+    """crc_update(crc, data, len) of the reference on host memory."""
+    buf = _as_bytes(data)
+    ptr = buf.ctypes.data if buf.size else None
+    return int(_lib.lib().crc_update(crc & 0xFFFFFFFFFFFFFFFF, ptr, buf.size))
+
+
+def crc32(data, seed=CRC_INIT):
+    """Finalized CRC-32 (zlib-compatible) of host bytes."""
+    return crc_finalize(crc_update(seed, data))
+
+
+def crc32_shift(raw_state, nbytes):
+    return int(_lib.lib().cio_crc32_shift(raw_state & 0xFFFFFFFF, nbytes))
+
+
+def crc32_combine(raw_a, raw0_b, len_b):
+    return int(_lib.lib().cio_crc32_combine(raw_a & 0xFFFFFFFF, raw0_b & 0xFFFFFFFF, len_b))
+
+
+def _u64_array(values):
+    arr = np.ascontiguousarray(np.asarray(values, dtype=np.uint64))
+    return arr, arr.ctypes.data_as(_lib.c_u64_p)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(int(stream.cuda_stream))
+
+
+class Crc32Plan:
+    """Geometry of one batch (chunk offsets/lengths relative to a base).
+
+    exec() enqueues the CRC kernels on a stream with no host synchronisation.
+    """
+
+    def __init__(self, offs, lens):
+        self._offs, po = _u64_array(offs)
+        self._lens, pl = _u64_array(lens)
+        if self._offs.shape != self._lens.shape:
+            raise ValueError("offs and lens must have the same length")
+        self.n = int(self._offs.size)
+        handle = ctypes.c_void_p()
+        _lib.check(_lib.lib().cio_crc32_plan_create(ctypes.byref(handle), po, pl, self.n),
+                   "cio_crc32_plan_create")
+        self._handle = handle
+
+    @property
+    def bytes(self):
+        return int(_lib.lib().cio_crc32_plan_bytes(self._handle))
+
+    def exec(self, base, out, seeds=None, stream=None):
+        """base: uint8 cuda tensor; out: int32/uint32 cuda tensor of n; seeds: same or None."""
+        _lib.check(_lib.lib().cio_crc32_plan_exec(self._handle, _ptr(base), _ptr(seeds), _ptr(out),
+                                                  _stream_ptr(stream)),
+                   "cio_crc32_plan_exec")
+
+    def exec_events(self, base, out, ev_start, ev_stop, seeds=None, stream=None):
+        """exec() with HIP events recorded around the main kernel only."""
+        _lib.check(_lib.lib().cio_crc32_plan_exec_events(self._handle, _ptr(base), _ptr(seeds),
+                                                         _ptr(out), _stream_ptr(stream),
+                                                         ev_start, ev_stop),
+                   "cio_crc32_plan_exec_events")
+
+    def close(self):
+        if getattr(self, "_handle", None):
+            _lib.lib().cio_crc32_plan_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def _to_u32_numpy(t):
+    return t.cpu().numpy().view(np.uint32).copy()
+
+
+def crc32_batch_dev(base, offs, lens, seeds=None, stream=None):
+    """Raw CRC state of every chunk of a device-resident batch (numpy uint32)."""
+    import torch
+    n = len(offs)
+    out = torch.empty(n, dtype=torch.int32, device=base.device)
+    seeds_t = None
+    if seeds is not None:
+        seeds_t = torch.from_numpy(np.asarray(seeds, dtype=np.uint32).view(np.int32)).to(base.device)
+    offs_arr = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    lens_arr = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    _lib.check(_lib.lib().cio_crc32_batch_dev(_ptr(base), offs_arr.ctypes.data_as(_lib.c_u64_p),
+                                              lens_arr.ctypes.data_as(_lib.c_u64_p), _ptr(seeds_t),
+                                              _ptr(out), n, _stream_ptr(stream)),
+               "cio_crc32_batch_dev")
+    return _to_u32_numpy(out)
+
+
+def crc32_batch_host(bufs, seeds=None):
+    """Raw CRC states of host buffers via pinned staging + H2D + GPU kernels."""
+    arrays = [_as_bytes(b) for b in bufs]
+    n = len(arrays)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data if a.size else None for a in arrays])
+    lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrays])
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    seeds_p = None
+    if seeds is not None:
+        seeds_arr = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint32))
+        seeds_p = seeds_arr.ctypes.data_as(_lib.c_u32_p)
+    _lib.check(_lib.lib().cio_crc32_batch_host(ptrs, lens, seeds_p,
+                                               out.ctypes.data_as(_lib.c_u32_p), n),
+               "cio_crc32_batch_host")
+    return out[:n]
+
+
+def fill_synthetic(base, offs, lens, seed, ids=None, stream=None):
+    """Fill chunks of a device buffer with the deterministic splitmix64 generator
+    (chunk i uses generator index ids[i], default i)."""
+    offs_arr = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    lens_arr = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    ids_p = None
+    if ids is not None:
+        ids_arr = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
+        assert ids_arr.shape == offs_arr.shape
+        ids_p = ids_arr.ctypes.data_as(_lib.c_u64_p)
+    _lib.check(_lib.lib().cio_gpu_fill_synthetic(_ptr(base), offs_arr.ctypes.data_as(_lib.c_u64_p),
+                                                 lens_arr.ctypes.data_as(_lib.c_u64_p), ids_p,
+                                                 len(offs_arr), seed, _stream_ptr(stream)),
+               "cio_gpu_fill_synthetic")
+
+
+def sha1_batch_dev(base, offs, lens, stream=None):
+    """SHA-1 digests (n x 20 bytes, numpy uint8) of a device-resident batch."""
+    import torch
+    n = len(offs)
+    out = torch.empty(max(n, 1) * 20, dtype=torch.uint8, device=base.device)
+    offs_arr = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    lens_arr = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    _lib.check(_lib.lib().cio_sha1_batch_dev(_ptr(base), offs_arr.ctypes.data_as(_lib.c_u64_p),
+                                             lens_arr.ctypes.data_as(_lib.c_u64_p), _ptr(out), n,
+                                             _stream_ptr(stream)),
+               "cio_sha1_batch_dev")
+    return out[: n * 20].cpu().numpy().reshape(n, 20)

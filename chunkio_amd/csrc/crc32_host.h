@@ -1,0 +1,32 @@
+/* Internal host-side declarations shared by the C and HIP translation units. */
+#ifndef CIOA_CRC32_HOST_H
+#define CIOA_CRC32_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CIOA_POLY 0xEDB88320u
+
+uint64_t cioa_crc_update_host(uint64_t crc, const void *data, size_t len);
+const uint32_t *cioa_byte_table(void);
+uint32_t cioa_multmodp(uint32_t a, uint32_t b);
+uint32_t cioa_xpow8n(uint64_t n);
+void cioa_gen_slice4(uint32_t out[4][256]);
+void cioa_gen_shift_table(uint32_t out[4][256], uint64_t dist);
+void cioa_gen_xpow8_table(uint32_t *out, size_t count, uint64_t unit_bytes);
+
+/* Record an error message for cio_gpu_last_error(); returns CIO_ERROR (-1). */
+int cioa_fail_msg(const char *what, const char *detail);
+
+uint32_t cio_crc32_shift(uint32_t raw_state, uint64_t nbytes);
+uint32_t cio_crc32_combine(uint32_t raw_a, uint32_t raw0_b, uint64_t len_b);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,150 @@
+/*
+ * cio_crc32_gpu.h -- C ABI of libchunkio_amd.so: batched CRC-32 (and SHA-1)
+ * over independent chunk content buffers on an MI355X (gfx950).
+ *
+ * Every entry point is plain C: pointers, sizes, and an opaque HIP stream
+ * passed as void* (NULL = the legacy default stream).  No torch or HIP types
+ * appear in the signatures.  Return codes follow chunkio's conventions
+ * (include/chunkio/chunkio.h:50-53): CIO_OK 0 / CIO_ERROR -1; the reason of
+ * the last failure on the calling thread is available from
+ * cio_gpu_last_error().
+ *
+ * What each call replaces in the reference (fluent/chunkio):
+ *
+ *   crc_update()                     deps/crc32/crc32.c:337-390, reached from
+ *                                    src/cio_file.c:92 and :110 (header
+ *                                    <crc32/crc32.h>, shipped in include/crc32)
+ *   cio_crc32_batch_dev()            N independent calls of
+ *   cio_crc32_plan_create/exec()     cio_file_calculate_checksum()
+ *                                    (src/cio_file.c:66-94), i.e. the loop
+ *                                    cio_scan_stream_files() drives through
+ *                                    cio_chunk_open -> cio_file_format_check
+ *                                    (src/cio_scan.c:105, src/cio_file.c:266-290)
+ *                                    for device-resident chunk contents
+ *   cio_crc32_batch_host()           the same over host (e.g. mmap'd) buffers:
+ *                                    pinned staging + H2D + kernel + D2H
+ *   cio_crc32_shift/_combine()       no reference counterpart; folds GPU partial
+ *                                    CRCs into a running cf->crc_cur
+ *                                    (src/cio_file.c:97-113)
+ *   cio_sha1_batch_dev()             cio_sha1_init/update/final over each chunk
+ *                                    (src/cio_sha1.c:91-122)
+ *
+ * CRC values in and out are RAW states (not finalized), exactly what
+ * crc_update() takes and returns: seed 0xffffffff (= crc_init()) gives the
+ * state that crc_finalize() turns into the standard CRC-32.
+ */
+#ifndef CIO_CRC32_GPU_H
+#define CIO_CRC32_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef CIO_OK
+#define CIO_OK       0
+#define CIO_ERROR   -1
+#endif
+
+/* ---- device / library state ------------------------------------------- */
+
+/* Initialise the device tables on the current HIP device (idempotent, thread
+ * safe).  Called implicitly by every GPU entry point. */
+int cio_gpu_init(void);
+
+/* Human-readable reason for the last CIO_ERROR on this thread ("" if none). */
+const char *cio_gpu_last_error(void);
+
+/* Library build identification (kernel variant, arch). */
+const char *cio_gpu_version(void);
+
+/* ---- CRC-32 math on the host (no device needed) ------------------------ */
+
+/* crc_update(s, zeros(n)) computed in O(log n): multiply by x^(8n) mod P. */
+uint32_t cio_crc32_shift(uint32_t raw_state, uint64_t nbytes);
+
+/* Raw state of A||B from raw0(A) (any seed), raw0(B) (ZERO-seeded raw
+ * state of B) and |B|:  crc_update(s, A||B) ==
+ *     cio_crc32_combine(crc_update(s, A), crc_update(0, B), |B|). */
+uint32_t cio_crc32_combine(uint32_t raw_a, uint32_t raw0_b, uint64_t len_b);
+
+/* ---- batched CRC-32, device-resident ----------------------------------- */
+
+/*
+ * A plan fixes the geometry of a batch (n chunks at byte offsets offs[i]
+ * with lengths lens[i] from one device base pointer) and uploads the work
+ * partition once; executing it is two kernel launches on `stream` with no
+ * host synchronisation, so it can be captured in a HIP graph.
+ * offs/lens are HOST arrays.  Offsets and lengths may be arbitrary (any byte
+ * alignment, zero-length chunks allowed).
+ */
+typedef struct cio_crc32_plan cio_crc32_plan;
+
+int  cio_crc32_plan_create(cio_crc32_plan **plan, const uint64_t *offs,
+                           const uint64_t *lens, size_t n);
+void cio_crc32_plan_destroy(cio_crc32_plan *plan);
+
+/* dev_seeds: device array of n raw seeds, or NULL for crc_init() each.
+ * dev_out:   device array of n raw CRC states (uint32).  */
+int  cio_crc32_plan_exec(const cio_crc32_plan *plan, const void *dev_base,
+                         const uint32_t *dev_seeds, uint32_t *dev_out,
+                         void *stream);
+
+/* Same as cio_crc32_plan_exec, recording HIP events (from
+ * cio_gpu_event_create) on `stream` immediately before and after the main
+ * CRC kernel, for roofline measurement of that kernel alone. */
+int  cio_crc32_plan_exec_events(const cio_crc32_plan *plan, const void *dev_base,
+                                const uint32_t *dev_seeds, uint32_t *dev_out,
+                                void *stream, void *ev_piece_start,
+                                void *ev_piece_stop);
+
+/* Total content bytes the plan covers (sum of lens). */
+uint64_t cio_crc32_plan_bytes(const cio_crc32_plan *plan);
+
+/* One-shot: plan + exec + wait + destroy. */
+int  cio_crc32_batch_dev(const void *dev_base, const uint64_t *offs,
+                         const uint64_t *lens, const uint32_t *dev_seeds,
+                         uint32_t *dev_out, size_t n, void *stream);
+
+/* ---- batched CRC-32 over host memory (end-to-end path) ----------------- */
+
+/* bufs[i]/lens[i]: host buffers (e.g. mmap'd chunk files, any alignment).
+ * seeds: host array or NULL.  out_raw: host array of raw states.
+ * Streams the batch through pinned staging buffers with H2D copies
+ * overlapped with the kernels; synchronous on return. */
+int  cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
+                          const uint32_t *seeds, uint32_t *out_raw, size_t n);
+
+/* ---- synthetic data (benchmarks / tests) ------------------------------- */
+
+/* Fill dev_base + offs[i] .. + lens[i] with the deterministic generator
+ *   word_k(id) = splitmix64(seed ^ (0x9E3779B97F4A7C15 * (id + 1)) + k)
+ * emitted little-endian (byte t of the chunk = byte t%8 of word_{t/8}(id)),
+ * id = ids[i] (host array) or i when ids is NULL.  Synchronous. */
+int  cio_gpu_fill_synthetic(void *dev_base, const uint64_t *offs,
+                            const uint64_t *lens, const uint64_t *ids, size_t n,
+                            uint64_t seed, void *stream);
+
+/* ---- batched SHA-1, device-resident ------------------------------------ */
+
+/* 20-byte digests (big-endian byte order, as SHA1_Final writes them) into
+ * dev_digests + 20*i.  offs/lens are HOST arrays. */
+int  cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs,
+                        const uint64_t *lens, uint8_t *dev_digests, size_t n,
+                        void *stream);
+
+/* ---- timing helpers (HIP events on a given stream) --------------------- */
+
+void  *cio_gpu_event_create(void);
+void   cio_gpu_event_destroy(void *ev);
+int    cio_gpu_event_record(void *ev, void *stream);
+float  cio_gpu_event_elapsed_ms(void *start, void *stop);   /* syncs stop */
+int    cio_gpu_stream_sync(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CIO_CRC32_GPU_H */

@@ -1,0 +1,80 @@
+"""C ABI of libchunkio_amd.so on the CPU: loads, exports every declared
+symbol, and its host-side math (crc_update, shift, combine) matches the
+oracle.  No GPU compute calls here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import chunkio_amd
+from chunkio_amd import _lib
+from oracle import pyoracle as po
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INIT = 0xFFFFFFFF
+
+
+def declared_functions():
+    names = set()
+    for hdr in ("include/crc32/crc32.h", "include/chunkio_amd/cio_crc32_gpu.h"):
+        text = open(os.path.join(ROOT, hdr)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^\s*(?!static|typedef|#)[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(",
+                             text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    decl = declared_functions()
+    assert "crc_update" in decl and "cio_crc32_plan_exec" in decl
+    missing = [n for n in sorted(decl) if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_lib.EXPORTS) >= decl, sorted(decl - set(_lib.EXPORTS))
+
+
+def test_version_string():
+    assert b"gfx950" in chunkio_amd.lib().cio_gpu_version()
+
+
+@pytest.mark.parametrize("seed", [0, INIT, 0xBE26ED00])
+def test_crc_update_matches_oracle(seed):
+    rng = np.random.default_rng(11)
+    buf = rng.integers(0, 256, 70000, dtype=np.uint8)
+    for n in list(range(0, 80)) + [127, 128, 129, 4095, 4096, 4097, 65536 + 3]:
+        for mis in (0, 1, 5, 15):
+            chunk = buf[mis:mis + n]
+            assert chunkio_amd.crc_update(seed, chunk) == po.crc_update(seed, chunk)
+
+
+def test_crc_update_kats(data400):
+    assert chunkio_amd.crc32(b"123456789") == 0xCBF43926
+    assert chunkio_amd.crc32(b"\0\0") == 0x41D912FF
+    assert chunkio_amd.crc32(b"\0\0" + data400) == 0x103CFA67
+    assert chunkio_amd.crc32(b"\0\0" + data400 * 5) == 0x088740E7
+    assert chunkio_amd.crc_update(INIT, b"") == INIT
+
+
+def test_crc_t_is_8_bytes():
+    # crc_t = uint_fast32_t is 8 bytes on LP64 Linux; cio_file.c:111 memcpy()s 8 bytes.
+    assert ctypes.sizeof(ctypes.c_uint64) == 8
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.crc_update
+    f.restype = ctypes.c_uint64
+    f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+    # upper bits of the state are masked off, as in crc32.c:389
+    assert f(0xFFFFFFFF00000000 | INIT, None, 0) == INIT
+
+
+def test_shift_and_combine_match_oracle():
+    rng = np.random.default_rng(12)
+    for n in [0, 1, 3, 64, 4032, 4096, 409600, 2 ** 32 + 5, 2 ** 40]:
+        s = int(rng.integers(0, 2 ** 32))
+        assert chunkio_amd.crc32_shift(s, n) == po.crc_shift(s, n)
+    a = rng.integers(0, 256, 1000, dtype=np.uint8)
+    b = rng.integers(0, 256, 777, dtype=np.uint8)
+    whole = po.crc_update(INIT, np.concatenate([a, b]))
+    assert chunkio_amd.crc32_combine(po.crc_update(INIT, a), po.crc_update(0, b), len(b)) == whole

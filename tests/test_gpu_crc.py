@@ -1,0 +1,229 @@
+"""GPU parity: batched device CRC-32 (through the C ABI) vs the oracle / golden.
+
+Bar: bit-exact raw CRC state for every chunk.  Sizes: the oracle runs on every
+chunk up to config-2 size (1024 x 400 KB); at config-3/4 sizes the tests use
+the golden samples plus size-independent properties (split-and-combine).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import chunkio_amd as cio
+from chunkio_amd import workloads as wl
+from oracle import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+INIT = 0xFFFFFFFF
+
+
+def to_dev(buf, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(buf)).to(cuda)
+
+
+def pack(chunks, misalign=None, gap=0):
+    """Place byte arrays in one buffer; chunk i starts at (16-aligned + misalign[i])."""
+    offs, pos = [], 0
+    for i, c in enumerate(chunks):
+        m = 0 if misalign is None else int(misalign[i])
+        pos = ((pos + 15) & ~15) + m
+        offs.append(pos)
+        pos += len(c) + gap
+    buf = np.zeros(pos + 64, dtype=np.uint8)
+    for o, c in zip(offs, chunks):
+        buf[o:o + len(c)] = np.frombuffer(bytes(c), dtype=np.uint8) if not isinstance(c, np.ndarray) else c
+    return buf, np.asarray(offs, np.uint64), np.asarray([len(c) for c in chunks], np.uint64)
+
+
+def gpu_crc(cuda, buf, offs, lens, seeds=None):
+    return cio.crc32_batch_dev(to_dev(buf, cuda), offs, lens, seeds=seeds)
+
+
+def test_kats(cuda, golden, data400):
+    from test_oracle import kat_bytes
+    chunks = [kat_bytes(k, data400) for k in golden["kats"]]
+    for mis in range(16):
+        buf, offs, lens = pack(chunks, misalign=[mis] * len(chunks))
+        got = gpu_crc(cuda, buf, offs, lens)
+        assert [int(x) for x in got] == [k["raw"] for k in golden["kats"]], mis
+
+
+def test_reference_fs_expectations(cuda, data400):
+    # tests/fs.c:201-214: "\0\0" -> 0x41D912FF, "\0\0" + 400kb.txt -> 0x103CFA67
+    buf, offs, lens = pack([b"\0\0", b"\0\0" + data400, b"\0\0" + data400 * 5], misalign=[6, 6, 6])
+    got = gpu_crc(cuda, buf, offs, lens) ^ np.uint32(INIT)
+    assert list(got) == [0x41D912FF, 0x103CFA67, 0x088740E7]
+
+
+def test_every_length_0_to_4096(cuda, golden):
+    g = golden["random_by_len"]
+    chunks = [wl.gen_chunk(g["seed"], n, n) for n in range(g["max_len"] + 1)]
+    for mis_mode in range(3):
+        mis = [(n * 7 + mis_mode) % 16 for n in range(len(chunks))]
+        buf, offs, lens = pack(chunks, misalign=mis)
+        got = gpu_crc(cuda, buf, offs, lens)
+        assert list(map(int, got)) == g["raw"]
+
+
+def test_packed_contiguous_arbitrary_alignment(cuda):
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 20000, 3000).astype(np.uint64)
+    buf, offs = wl.host_batch(0x77, lens)
+    want = po.crc_batch(buf, offs, lens)
+    got = gpu_crc(cuda, buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_step_boundary_lengths_and_misalignments(cuda):
+    lens = [4, 5, 6, 7, 8, 15, 16, 17, 63, 64, 65, 127, 128, 4031, 4032, 4033, 4095, 4096, 4097,
+            4111, 8176, 8191, 8192, 8193, 12287, 12288, 12289, 65535, 65536, 65537, 262143, 409600]
+    chunks, mis = [], []
+    for m in range(16):
+        for n in lens:
+            chunks.append(wl.gen_chunk(0x99, len(chunks), n))
+            mis.append(m)
+    buf, offs, ln = pack(chunks, misalign=mis)
+    want = po.crc_batch(buf, offs, ln)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, ln), want)
+
+
+def test_seeds(cuda, golden):
+    g = golden["seeded"]
+    chunks = [wl.gen_chunk(g["data_seed"], v["len"], v["len"]) for v in g["vectors"]]
+    seeds = np.asarray([v["seed"] for v in g["vectors"]], np.uint32)
+    buf, offs, lens = pack(chunks, misalign=[i % 16 for i in range(len(chunks))])
+    got = gpu_crc(cuda, buf, offs, lens, seeds=seeds)
+    assert list(map(int, got)) == [v["raw"] for v in g["vectors"]]
+
+
+def test_tiny_and_empty_chunks_with_seeds(cuda):
+    rng = np.random.default_rng(6)
+    chunks = [rng.integers(0, 256, n, dtype=np.uint8) for n in [0, 1, 2, 3, 0, 3, 4, 1] * 20]
+    seeds = rng.integers(0, 2 ** 32, len(chunks), dtype=np.uint64).astype(np.uint32)
+    buf, offs, lens = pack(chunks, misalign=rng.integers(0, 16, len(chunks)))
+    want = po.crc_batch(buf, offs, lens, seeds=seeds)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds), want)
+    # empty batch
+    assert len(gpu_crc(cuda, np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint64))) == 0
+
+
+def test_zero_and_constant_data(cuda):
+    # all-zero (the LDS tables' best case) and all-0xFF buffers, many sizes
+    chunks = [np.zeros(n, np.uint8) for n in (4, 100, 4096, 70001)] + \
+             [np.full(n, 0xFF, np.uint8) for n in (4, 100, 4096, 70001)]
+    buf, offs, lens = pack(chunks, misalign=[3] * len(chunks))
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
+
+
+def test_more_chunks_than_waves(cuda):
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 400, 20000).astype(np.uint64)
+    buf, offs = wl.host_batch(0x1234, lens)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
+
+
+def test_one_huge_chunk_spans_all_waves(cuda):
+    n = 48 * 1024 * 1024 + 12345
+    data = wl.gen_chunk(0xBEEF, 0, n)
+    buf, offs, lens = pack([data], misalign=[9])
+    for seed in (INIT, 0, 0xDEADBEEF):
+        got = gpu_crc(cuda, buf, offs, lens, seeds=np.asarray([seed], np.uint32))
+        assert int(got[0]) == po.crc_update(seed, data)
+
+
+def test_plan_reuse_on_stream(cuda):
+    import torch
+    lens = wl.cfg2_lens(64)
+    offs = wl.packed_offsets(lens)
+    total = wl.batch_bytes(offs, lens)
+    a = torch.empty(total, dtype=torch.uint8, device=cuda)
+    b = torch.empty(total, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(a, offs, lens, wl.CFG2_SEED)
+    cio.fill_synthetic(b, offs, lens, 0x5555)
+    out = torch.empty(64, dtype=torch.int32, device=cuda)
+    with cio.Crc32Plan(offs, lens) as plan:
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            for buf, seed in ((a, wl.CFG2_SEED), (b, 0x5555), (a, wl.CFG2_SEED)):
+                plan.exec(buf, out, stream=s)
+                s.synchronize()
+                got = out.cpu().numpy().view(np.uint32)
+                want = po.crc_batch_chunks(seed, lens, idx=range(4))
+                np.testing.assert_array_equal(got[:4], want)
+
+
+def test_fill_matches_numpy_generator(cuda):
+    import torch
+    rng = np.random.default_rng(8)
+    lens = rng.integers(0, 5000, 300).astype(np.uint64)
+    buf, offs = wl.host_batch(0xF00D, lens)
+    dev = torch.zeros(len(buf), dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, 0xF00D)
+    np.testing.assert_array_equal(dev.cpu().numpy(), buf)
+
+
+def test_cfg2_full_batch_golden(cuda, golden):
+    import torch
+    g = golden["cfg2"]
+    lens = wl.cfg2_lens()
+    offs = wl.packed_offsets(lens)
+    dev = torch.empty(wl.batch_bytes(offs, lens), dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, g["seed"])
+    got = cio.crc32_batch_dev(dev, offs, lens)
+    assert list(map(int, got[:32])) == g["first32"]
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_of_raw_le"]
+
+
+def split_combine_check(cuda, dev, offs, lens, want_full):
+    """Size-independent property: CRC each chunk as two parts, fold on the host."""
+    rng = np.random.default_rng(9)
+    cut = (rng.random(len(lens)) * lens.astype(np.float64)).astype(np.uint64)
+    offs2 = np.concatenate([offs, offs + cut])
+    lens2 = np.concatenate([cut, lens - cut])
+    seeds2 = np.concatenate([np.full(len(lens), INIT, np.uint32), np.zeros(len(lens), np.uint32)])
+    parts = cio.crc32_batch_dev(dev, offs2, lens2, seeds=seeds2)
+    n = len(lens)
+    for i in range(0, n, max(1, n // 2000)):
+        folded = cio.crc32_combine(int(parts[i]), int(parts[n + i]), int(lens2[n + i]))
+        assert folded == int(want_full[i]), i
+
+
+def test_cfg3_mixed_sizes_full(cuda, golden):
+    import torch
+    g = golden["cfg3"]
+    lens = wl.cfg3_lens()
+    offs = wl.packed_offsets(lens)          # contiguous: arbitrary chunk alignment
+    dev = torch.empty(wl.batch_bytes(offs, lens) + 16, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, g["seed"])
+    got = cio.crc32_batch_dev(dev, offs, lens)
+    assert [int(got[i]) for i in g["sample_idx"]] == g["sample_raw"]
+    split_combine_check(cuda, dev, offs, lens, got)
+
+
+def test_cfg4_shard_golden(cuda, golden):
+    import torch
+    g = golden["cfg4"]
+    idx = np.arange(64)                       # first 64 chunks (one GPU of a G=128 split)
+    lens = wl.cfg4_lens()[idx]
+    offs = wl.packed_offsets(lens)
+    dev = torch.empty(wl.batch_bytes(offs, lens), dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, g["seed"])
+    got = cio.crc32_batch_dev(dev, offs, lens)
+    assert list(map(int, got[:8])) == g["sample_raw"]
+    split_combine_check(cuda, dev, offs, lens, got)
+
+
+def test_host_batch_end_to_end(cuda, data400):
+    rng = np.random.default_rng(10)
+    bufs = [np.frombuffer(b"\0\0" + data400, np.uint8)]
+    bufs += [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(0, 300000, 200)]
+    big = rng.integers(0, 256, 150 * 1024 * 1024 + 7, dtype=np.uint8)   # spans 3 staging groups
+    bufs += [big[1:]]                                                   # misaligned host view
+    bufs += [np.zeros(0, np.uint8), np.frombuffer(b"abc", np.uint8)]
+    seeds = rng.integers(0, 2 ** 32, len(bufs), dtype=np.uint64).astype(np.uint32)
+    got = cio.crc32_batch_host(bufs, seeds=seeds)
+    want = [po.crc_update(int(s), b) for s, b in zip(seeds, bufs)]
+    assert list(map(int, got)) == want
+    got0 = cio.crc32_batch_host(bufs[:1])
+    assert int(got0[0]) ^ INIT == 0x103CFA67

@@ -1,0 +1,123 @@
+"""CPU model of the GPU kernel's decomposition (host logic; no GPU).
+
+Re-plays, in Python, exactly the work split of crc32_gpu.hip -- plan
+construction (virtual aligned chunks, wave-steps, even split over W waves,
+first chunk per wave), per-lane 64-byte blocks with the 4032-byte step shift,
+head zeroing + seed fold, partial last steps, per-lane shift to the piece end,
+piece slots (wave + chunk) and the finisher's Horner fold -- using the oracle
+for the per-lane byte CRCs and GF(2) shifts.  Any index slip in that scheme
+shows up here as a CRC mismatch against crc_update on the whole chunk.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+
+STEP, BPL, WAVE = 4096, 64, 64
+INIT = 0xFFFFFFFF
+
+
+def plan(offs, lens, W):
+    desc, S = [], 0
+    for o, n in zip(offs, lens):
+        h = o & 15
+        vlen = h + n
+        ns = (vlen + STEP - 1) // STEP if n >= 4 else 0
+        desc.append(dict(a=o - h, h=h, vlen=vlen, g=S, nsteps=ns))
+        S += ns
+    wc, c = [], 0
+    for w in range(W):
+        g0 = (w * S) // W if S else 0
+        while c < len(desc) and (desc[c]["nsteps"] == 0 or desc[c]["g"] + desc[c]["nsteps"] <= g0):
+            c += 1
+        wc.append(min(c, len(desc) - 1))
+    return desc, S, wc
+
+
+def lane_block(buf, d, jj, lane, seed):
+    """Bytes of lane `lane` at step jj (virtual chunk, head zeroed, seed folded)."""
+    bstart = jj * STEP + lane * BPL
+    vb = 0 if bstart >= d["vlen"] else min(d["vlen"] - bstart, BPL)
+    blk = np.array(buf[d["a"] + bstart: d["a"] + bstart + vb], dtype=np.uint8)
+    if jj == 0 and lane == 0 and vb:
+        blk[:d["h"]] = 0
+        sb = np.frombuffer(int(seed).to_bytes(4, "little"), np.uint8)
+        blk[d["h"]:d["h"] + 4] ^= sb
+    return bstart, vb, blk
+
+
+def model(buf, offs, lens, seeds, W):
+    desc, S, wc = plan(offs, lens, W)
+    partials = {}
+    start = lambda w: (w * S) // W  # noqa: E731
+    for w in range(W):
+        g, gend = start(w), start(w + 1)
+        if g >= gend:
+            continue
+        c = wc[w]
+        d = desc[c]
+        j = g - d["g"]
+        while True:
+            jend = min(d["nsteps"], j + (gend - g))
+            s = [0] * WAVE
+            lane_end = [0] * WAVE
+            for jj in range(j, jend):
+                for lane in range(WAVE):
+                    bstart, vb, blk = lane_block(buf, d, jj, lane, seeds[c] if jj == 0 else 0)
+                    if vb == 0:
+                        continue
+                    st = po.crc_shift(s[lane], STEP - BPL)     # step shift (any state)
+                    s[lane] = po.crc_update(st, blk)
+                    lane_end[lane] = bstart + vb
+            pend = min(jend * STEP, d["vlen"])
+            acc = 0
+            for lane in range(WAVE):
+                if s[lane]:
+                    dist = max(0, pend - lane_end[lane])
+                    assert dist < 2 * STEP
+                    acc ^= po.crc_shift(s[lane], dist)
+            slot = w + c
+            assert slot not in partials
+            partials[slot] = acc
+            g += jend - j
+            if g >= gend:
+                break
+            c += 1
+            while desc[c]["nsteps"] == 0:
+                c += 1
+            d = desc[c]
+            j = 0
+    # finisher
+    wave_of = lambda gg: ((gg + 1) * W + S - 1) // S - 1  # noqa: E731
+    out = []
+    for c, d in enumerate(desc):
+        if d["nsteps"] == 0:
+            out.append(po.crc_update(seeds[c], buf[offs[c]:offs[c] + lens[c]]))
+            continue
+        w0, w1 = wave_of(d["g"]), wave_of(d["g"] + d["nsteps"] - 1)
+        acc = partials[w0 + c]
+        for w in range(w0 + 1, w1 + 1):
+            st, en = start(w), start(w + 1)
+            if st == en:
+                continue
+            ps, pe = st - d["g"], min(en - d["g"], d["nsteps"])
+            nb = d["vlen"] - ps * STEP if w == w1 else (pe - ps) * STEP
+            acc = po.crc_shift(acc, nb) ^ partials[w + c]
+        out.append(acc)
+    return out
+
+
+@pytest.mark.parametrize("W", [1, 3, 8, 64])
+def test_model_matches_crc_update(W):
+    rng = np.random.default_rng(W)
+    lens = [0, 1, 3, 4, 5, 63, 64, 65, 4095, 4096, 4097, 8200, 13000, 2, 9000, 0, 30000]
+    offs, pos = [], 0
+    for n in lens:
+        pos = ((pos + 15) & ~15) + int(rng.integers(0, 16))
+        offs.append(pos)
+        pos += n
+    buf = rng.integers(0, 256, pos + 32, dtype=np.uint8)
+    seeds = [int(x) for x in rng.integers(0, 2 ** 32, len(lens))]
+    got = model(buf, offs, lens, seeds, W)
+    want = [po.crc_update(s, buf[o:o + n]) for s, o, n in zip(seeds, offs, lens)]
+    assert got == want

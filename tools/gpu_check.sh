@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU session: parity tests, bench, rocprofv3 kernel trace.  Each GPU step
+# has its own time limit; the script stops at the first fault/timeout.
+# Usage (from the repo root, on the GPU box): bash tools/gpu_check.sh [tag]
+set -u
+TAG=${1:-r01}
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+stop_if_fatal() {   # rc of a GPU step: 0 ok, 1 test failures (keep going), else stop
+  local rc=$1 what=$2
+  echo "[$what] rc=$rc"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "fatal rc in $what, stopping"; exit "$rc"; fi
+}
+rocm-smi --showproductname > $OUT/gpu_info.txt 2>&1 || true
+timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1
+stop_if_fatal $? pytest
+tail -5 $OUT/pytest_gpu_$TAG.log
+timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+stop_if_fatal $? bench
+cat $OUT/bench_$TAG.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- \
+    python3 bench.py --steps 20 --warmup 3 --no-cpu > $OUT/bench_prof_$TAG.json 2> $OUT/rocprof_$TAG.err
+stop_if_fatal $? rocprof
+find $OUT/prof_$TAG -name "*stats*" | head
