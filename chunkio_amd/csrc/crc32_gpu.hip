@@ -47,26 +47,32 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kBPL = 64;                    // bytes per lane per step
-constexpr int kStep = kWave * kBPL;         // 4096 bytes per wave-step
+constexpr int kGran = 16;                   // bytes per lane per sub-chain per step
+constexpr int kSub = 4;                     // sub-chains per lane
+constexpr int kRow = kWave * kGran;         // 1024: one coalesced wave-instruction
+constexpr int kStep = kSub * kRow;          // 4096 bytes per wave-step
 constexpr int kThreads = 1024;              // one workgroup per CU
 constexpr int kWavesPerWG = kThreads / kWave;
 constexpr int kX8Count = 2 * kStep;         // x^(8m), m in [0, 8192)
 constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
-constexpr uint32_t kShiftWordOff = kSliceBytes / 4;
-constexpr uint32_t kLdsWords = (kSliceBytes + 4096) / 4;
+constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
+constexpr uint32_t kShiftOff = kSliceBytes;
+constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
 
 struct ChunkDesc {
     uint64_t a;        // aligned-down start offset from the batch base
     uint64_t vlen;     // virtual length = (off & 15) + len
     uint64_t g;        // first global wave-step of this chunk
-    uint32_t nsteps;   // ceil(vlen / kStep); 0 for chunks handled by the finisher
+    uint32_t nsteps;   // ceil(vlen / kStep); 0 for tiny chunks (len < 4)
     uint32_t h;        // off & 15 (zeroed head bytes)
+    uint32_t npieces;  // waves holding a piece of this chunk
+    uint32_t pad[3];
 };
-static_assert(sizeof(ChunkDesc) == 32, "desc layout");
+static_assert(sizeof(ChunkDesc) == 48, "desc layout");
 
 // ---------------------------------------------------------------- device math
 
+// a(x) * b(x) mod P(x), reflected bit order (bit 31 = x^0).
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b)
 {
     uint32_t p = 0;
@@ -88,202 +94,131 @@ __device__ __forceinline__ uint64_t wave_of_step(uint64_t g, uint64_t S, uint64_
     return ((g + 1) * W + S - 1) / S - 1;
 }
 
-// Slice-table lookup in the replicated LDS image.
+// Slice tables in LDS, replicated 32x so lane l always reads bank (l & 31):
 //   byte address(k, b, lane) = (k>>1)*65536 + b*256 + (k&1)*128 + (lane&31)*4
+// One v_perm_b32 builds the address: {0, k>>1, x.byte, lane*4}.  lbase_hi =
+// lane*4 | 0x10000 selects tables 2-3, lbase_lo = lane*4 tables 0-1; (k&1)*128
+// is the instruction's immediate offset.
 template <int K>
-__device__ __forceinline__ uint32_t tl(const uint32_t *lds, uint32_t lb, uint32_t b)
+__device__ __forceinline__ uint32_t tl(const char *lds, uint32_t lbase, uint32_t x, int byte)
 {
-    const char *p = reinterpret_cast<const char *>(lds) + ((K >> 1) << 16) + ((K & 1) << 7);
-    return *reinterpret_cast<const uint32_t *>(p + ((b << 8) | lb));
+    const uint32_t sel = 0x0c020000u | ((4u + (uint32_t) byte) << 8);
+    const uint32_t addr = __builtin_amdgcn_perm(x, lbase, sel);
+    return *reinterpret_cast<const uint32_t *>(lds + addr + ((K & 1) << 7));
 }
 
-// crc_update(s, 4 little-endian bytes of w)
-__device__ __forceinline__ uint32_t word_step(const uint32_t *lds, uint32_t lb, uint32_t s, uint32_t w)
+// crc_update(s, 4 little-endian bytes of w):
+//   s' = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3],  x = s ^ w,  Tk = shift by k+1 bytes
+__device__ __forceinline__ uint32_t word_step(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
+                                              uint32_t s, uint32_t w)
 {
     const uint32_t x = s ^ w;
-    return tl<3>(lds, lb, x & 0xffu) ^ tl<2>(lds, lb, (x >> 8) & 0xffu) ^
-           tl<1>(lds, lb, (x >> 16) & 0xffu) ^ tl<0>(lds, lb, x >> 24);
+    return tl<3>(lds, lb_hi, x, 0) ^ tl<2>(lds, lb_hi, x, 1) ^
+           tl<1>(lds, lb_lo, x, 2) ^ tl<0>(lds, lb_lo, x, 3);
 }
 
-__device__ __forceinline__ uint32_t byte_step(const uint32_t *lds, uint32_t lb, uint32_t s, uint32_t byte)
+__device__ __forceinline__ uint32_t byte_step(const char *lds, uint32_t lb_lo, uint32_t s, uint32_t byte)
 {
-    return tl<0>(lds, lb, (s ^ byte) & 0xffu) ^ (s >> 8);
+    return tl<0>(lds, lb_lo, (s ^ byte) & 0xffu, 0) ^ (s >> 8);
 }
 
-// shift(s, kStep - kBPL): jump over the other lanes' bytes of one step.
-__device__ __forceinline__ uint32_t step_shift(const uint32_t *lds, uint32_t s)
+// shift(s, kStep - kGran): jump a sub-chain over the 4080 bytes between its
+// 16-byte blocks in consecutive steps.  8 replicas: address k*8192 + b*32 + (lane&7)*4.
+__device__ __forceinline__ uint32_t step_shift(const char *lds, uint32_t lrep, uint32_t s)
 {
-    const uint32_t *sh = lds + kShiftWordOff;
-    return sh[s & 0xffu] ^ sh[256 + ((s >> 8) & 0xffu)] ^
-           sh[512 + ((s >> 16) & 0xffu)] ^ sh[768 + (s >> 24)];
+    const char *t = lds + kShiftOff + lrep;
+    return *reinterpret_cast<const uint32_t *>(t + (s & 0xffu) * 32u) ^
+           *reinterpret_cast<const uint32_t *>(t + 8192 + ((s >> 8) & 0xffu) * 32u) ^
+           *reinterpret_cast<const uint32_t *>(t + 16384 + ((s >> 16) & 0xffu) * 32u) ^
+           *reinterpret_cast<const uint32_t *>(t + 24576 + (s >> 24) * 32u);
 }
 
-__device__ __forceinline__ uint32_t block64(const uint32_t *lds, uint32_t lb, uint32_t s,
-                                            const uint4 &v0, const uint4 &v1,
-                                            const uint4 &v2, const uint4 &v3)
+__device__ __forceinline__ uint32_t block16(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
+                                            uint32_t s, const uint4 &v)
 {
-    s = word_step(lds, lb, s, v0.x); s = word_step(lds, lb, s, v0.y);
-    s = word_step(lds, lb, s, v0.z); s = word_step(lds, lb, s, v0.w);
-    s = word_step(lds, lb, s, v1.x); s = word_step(lds, lb, s, v1.y);
-    s = word_step(lds, lb, s, v1.z); s = word_step(lds, lb, s, v1.w);
-    s = word_step(lds, lb, s, v2.x); s = word_step(lds, lb, s, v2.y);
-    s = word_step(lds, lb, s, v2.z); s = word_step(lds, lb, s, v2.w);
-    s = word_step(lds, lb, s, v3.x); s = word_step(lds, lb, s, v3.y);
-    s = word_step(lds, lb, s, v3.z); s = word_step(lds, lb, s, v3.w);
+    s = word_step(lds, lb_lo, lb_hi, s, v.x);
+    s = word_step(lds, lb_lo, lb_hi, s, v.y);
+    s = word_step(lds, lb_lo, lb_hi, s, v.z);
+    s = word_step(lds, lb_lo, lb_hi, s, v.w);
     return s;
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Streaming loads: non-temporal (read once).  With the coalesced layout (a
+// wave-instruction reads 1 KiB contiguous) this is the fastest HBM read
+// policy measured on MI355X (tools/probe/crc_probe.hip).
 __device__ __forceinline__ uint4 ldg16(const uint8_t *p)
 {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// Generic step: partial blocks, first step of a chunk (head zeroing + seed fold).
-__device__ __forceinline__ void slow_step(const uint32_t *lds, uint32_t lb, const uint8_t *cbase,
-                                       uint64_t jj, uint64_t vlen, uint32_t h, uint32_t seed,
-                                       uint32_t lane, uint32_t &s, uint64_t &lane_end)
+// One lane's 4 x 16 bytes of a step: sub-chain q holds [1024 q + 16 lane, +16).
+struct StepRegs {
+    uint4 q[kSub];
+};
+
+// Issue the 4 coalesced 16-byte loads of lane `lane` for step jj of a chunk.
+// Each granule address is clamped to the last 16-byte granule holding content
+// (a no-op except in a chunk's partial last step): addresses stay inside the
+// chunk's pages and every call is one straight-line path of exactly 4 loads,
+// so the compiler's vmcnt bookkeeping stays exact across the ring.
+__device__ __forceinline__ void load_step(StepRegs &r, const uint8_t *cbase, uint64_t jj,
+                                          uint64_t vlen, uint32_t lane)
 {
-    const uint64_t bstart = jj * kStep + (uint64_t) lane * kBPL;
-    const uint32_t vb = bstart >= vlen ? 0u : (uint32_t) min(vlen - bstart, (uint64_t) kBPL);
-    if (vb == 0) {
-        return;
-    }
-    uint32_t w[16];
-    const uint8_t *p = cbase + bstart;
+    const uint64_t b0 = jj * kStep + (uint64_t) lane * kGran;
+    const uint64_t last = (vlen - 1) & ~15ull;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if ((uint32_t) (q * 16) < vb) {
-            v = *reinterpret_cast<const uint4 *>(p + q * 16);
-        }
-        w[4 * q + 0] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    for (int q = 0; q < kSub; ++q) {
+        r.q[q] = ldg16(cbase + min(b0 + (uint64_t) q * kRow, last));
     }
-    if (jj == 0 && lane == 0) {
-        // Zero the alignment head [0, h) and fold the seed into bytes [h, h+4).
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int off = 4 * i - (int) h;
-            if (off <= -4) {
-                w[i] = 0u;
-            } else if (off < 0) {
-                w[i] = (w[i] & (~0u << (8 * -off))) ^ (seed << (8 * -off));
-            } else if (off == 0) {
-                w[i] ^= seed;
-            } else if (off < 4) {
-                w[i] ^= seed >> (8 * off);
-            }
-        }
-    }
-    s = step_shift(lds, s);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if ((uint32_t) (4 * i + 4) <= vb) {
-            s = word_step(lds, lb, s, w[i]);
-        } else if ((uint32_t) (4 * i) < vb) {
-            for (uint32_t t = 4 * i; t < vb; ++t) {
-                s = byte_step(lds, lb, s, (w[i] >> (8 * (t - 4 * i))) & 0xffu);
-            }
-        }
-    }
-    lane_end = bstart + vb;
 }
 
-__global__ void __launch_bounds__(kThreads, 1)
-crc32_piece_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restrict__ desc,
-                   const uint32_t *__restrict__ wave_chunk0, const uint32_t *__restrict__ seeds,
-                   uint32_t *__restrict__ partials, const uint32_t *__restrict__ g_slice,
-                   const uint32_t *__restrict__ g_shift, const uint32_t *__restrict__ g_x8,
-                   const uint32_t *__restrict__ cid, uint64_t S, uint32_t W, uint32_t n)
+// Generic step: partial blocks at a chunk end, and the first step of a chunk
+// (alignment-head zeroing + seed fold into content bytes 0..3, which can
+// straddle lanes 0 and 1 of sub-chain 0).
+__device__ __forceinline__ void slow_compute(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
+                                             uint32_t lrep, const StepRegs &r, uint64_t jj,
+                                             uint64_t vlen, uint32_t h, uint32_t seed, uint32_t lane,
+                                             uint32_t (&s)[kSub], uint64_t (&e)[kSub])
 {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords];
-    const uint32_t tid = threadIdx.x;
-
-    {   // Build the replicated slice tables and the step-shift table.
-        const uint32_t k = tid >> 8, b = tid & 255u;
-        const uint32_t v = g_slice[tid];
-        const uint4 v4 = make_uint4(v, v, v, v);
-        uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) +
-                                               ((k >> 1) << 16) + (b << 8) + ((k & 1u) << 7));
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            dst[q] = v4;
+    for (int q = 0; q < kSub; ++q) {
+        const uint64_t bs = jj * kStep + (uint64_t) q * kRow + (uint64_t) lane * kGran;
+        const uint32_t vb = bs >= vlen ? 0u : (uint32_t) min(vlen - bs, (uint64_t) kGran);
+        if (vb == 0) {
+            continue;
         }
-        lds[kShiftWordOff + tid] = g_shift[tid];
-    }
-    __syncthreads();
-
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (tid >> 6));
-    const uint32_t lane = tid & 63u;
-    const uint32_t lb = (lane & 31u) << 2;
-
-    uint64_t g = wave_start(wave, S, W);
-    const uint64_t gend = wave_start((uint64_t) wave + 1, S, W);
-    if (g >= gend) {
-        return;
-    }
-    uint32_t c = wave_chunk0[wave];
-    ChunkDesc d = desc[c];
-    uint64_t j = g - d.g;
-
-    for (;;) {
-        const uint64_t jend = min((uint64_t) d.nsteps, j + (gend - g));
-        const uint64_t full_end = d.vlen / kStep;
-        const uint8_t *cbase = base + d.a;
-        const uint32_t seed = (j == 0) ? (seeds ? seeds[cid ? cid[c] : c] : 0xffffffffu) : 0u;
-        uint32_t s = 0;
-        uint64_t lane_end = 0;
-        uint64_t jj = j;
-
-        if (jj == 0) {
-            slow_step(lds, lb, cbase, 0, d.vlen, d.h, seed, lane, s, lane_end);
-            jj = 1;
-        }
-        const uint64_t fe = min(jend, full_end);
-        if (jj < fe) {
-            const uint8_t *lp = cbase + jj * kStep + lane * kBPL;
-            uint4 c0 = ldg16(lp), c1 = ldg16(lp + 16), c2 = ldg16(lp + 32), c3 = ldg16(lp + 48);
-            for (; jj < fe; ++jj) {
-                uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
-                if (jj + 1 < fe) {
-                    lp += kStep;
-                    n0 = ldg16(lp); n1 = ldg16(lp + 16); n2 = ldg16(lp + 32); n3 = ldg16(lp + 48);
+        uint32_t w[4] = {r.q[q].x, r.q[q].y, r.q[q].z, r.q[q].w};
+        if (q == 0 && jj == 0 && lane < 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int off = (int) (16 * lane) + 4 * i - (int) h;
+                if (off <= -4) {
+                    w[i] = 0u;
+                } else if (off < 0) {
+                    w[i] = (w[i] & (~0u << (8 * -off))) ^ (seed << (8 * -off));
+                } else if (off == 0) {
+                    w[i] ^= seed;
+                } else if (off < 4) {
+                    w[i] ^= seed >> (8 * off);
                 }
-                s = step_shift(lds, s);
-                s = block64(lds, lb, s, c0, c1, c2, c3);
-                c0 = n0; c1 = n1; c2 = n2; c3 = n3;
             }
-            lane_end = (fe - 1) * kStep + (uint64_t) (lane + 1) * kBPL;
         }
-        if (jj < jend) {
-            slow_step(lds, lb, cbase, jj, d.vlen, d.h, 0u, lane, s, lane_end);
-        }
-
-        // Shift every lane's state to the piece end, XOR-reduce over the wave.
-        const uint64_t pend = min(jend * kStep, d.vlen);
-        const uint64_t dist = lane_end < pend ? pend - lane_end : 0;
-        uint32_t contrib = s ? multmodp(g_x8[min(dist, (uint64_t) (kX8Count - 1))], s) : 0u;
+        uint32_t st = step_shift(lds, lrep, s[q]);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            contrib ^= __shfl_xor(contrib, o);
-        }
-        if (lane == 0) {
-            partials[(uint64_t) wave + c] = contrib;
-        }
-
-        g += jend - j;
-        if (g >= gend) {
-            break;
-        }
-        do {
-            if (++c >= n) {
-                return;     // unreachable for a consistent plan; never read past desc[n-1]
+        for (int i = 0; i < 4; ++i) {
+            if ((uint32_t) (4 * i + 4) <= vb) {
+                st = word_step(lds, lb_lo, lb_hi, st, w[i]);
+            } else if ((uint32_t) (4 * i) < vb) {
+                for (uint32_t t = 4 * i; t < vb; ++t) {
+                    st = byte_step(lds, lb_lo, st, (w[i] >> (8 * (t - 4 * i))) & 0xffu);
+                }
             }
-            d = desc[c];
-        } while (d.nsteps == 0);
-        j = 0;
+        }
+        s[q] = st;
+        e[q] = bs + vb;
     }
 }
 
@@ -294,45 +229,295 @@ __device__ __forceinline__ uint32_t xpow8_bytes(uint64_t bytes, const uint32_t *
     return m == 0 ? x8[r] : multmodp(x4k[m], x8[r]);
 }
 
-__global__ void __launch_bounds__(256)
-crc32_finish_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restrict__ desc,
-                    const uint32_t *seeds, const uint32_t *__restrict__ partials,
-                    uint32_t *out, const uint32_t *__restrict__ g_byte,
-                    const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_x4k,
-                    const uint32_t *__restrict__ cid, uint64_t S, uint32_t W, uint32_t n)
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) {
-        return;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        v ^= __shfl_xor(v, o);
     }
-    const uint32_t oc = cid ? cid[c] : c;   // output / seed slot
-    const ChunkDesc d = desc[c];
-    if (d.nsteps == 0) {
-        // Tiny (len < 4) or empty chunk: byte-serial with the seed directly.
-        uint32_t s = seeds ? seeds[oc] : 0xffffffffu;
+    return v;
+}
+
+// All pieces of chunk c folded into one raw CRC by the last wave to publish
+// one: XOR over pieces of shift(piece, bytes after it), lanes in parallel.
+__device__ __forceinline__ void fold_chunk(const ChunkDesc &d, uint32_t c, uint32_t oc, uint32_t lane,
+                                           const unsigned long long *partials, uint32_t *out,
+                                           uint32_t *counters, const uint32_t *g_x8,
+                                           const uint32_t *g_x4k, uint64_t S, uint32_t W)
+{
+    const uint64_t w0 = wave_of_step(d.g, S, W);
+    const uint64_t w1 = wave_of_step(d.g + d.nsteps - 1, S, W);
+    uint32_t acc = 0;
+    for (uint64_t wb = w0; wb <= w1; wb += kWave) {
+        const uint64_t wv = wb + lane;
+        if (wv <= w1) {
+            const uint64_t st = wave_start(wv, S, W), en = wave_start(wv + 1, S, W);
+            if (st < en) {
+                const uint32_t p = (uint32_t) __hip_atomic_load(&partials[wv + c], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t pend = min(min(en - d.g, (uint64_t) d.nsteps) * kStep, d.vlen);
+                acc ^= p ? multmodp(xpow8_bytes(d.vlen - pend, g_x8, g_x4k), p) : 0u;
+            }
+        }
+    }
+    acc = wave_xor(acc);
+    if (lane == 0) {
+        out[oc] = acc;
+        __hip_atomic_store(&counters[c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// The CRC kernel: one launch per batch.
+//   1. every workgroup builds the LDS tables (160 KiB);
+//   2. every wave streams its even share of the batch's wave-steps through a
+//      D-deep register ring (loads for step g+D issued while step g is CRC'd),
+//      publishing one partial CRC per chunk piece;
+//   3. the last wave to publish a piece of a chunk folds the chunk;
+//   4. chunks shorter than 4 bytes are done byte-serially.
+// Rotate this wave's issue priority so that, over any 4 consecutive ring
+// iterations, every wave of a SIMD holds each priority level once: the
+// hardware's age tie-break otherwise lets the oldest wave of each SIMD run
+// ~30% ahead of the youngest, and the workgroup ends with the youngest.
+__device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
+{
+    switch ((slot_group + (uint32_t) it) & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
+template <int D, bool STAMPS = false, int PRIO = 1>
+__global__ void __launch_bounds__(kThreads, 1)
+crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restrict__ desc,
+                    const uint32_t *__restrict__ wave_chunk0, const uint32_t *__restrict__ tiny,
+                    const uint32_t *__restrict__ seeds, uint32_t *out, const uint32_t *__restrict__ cid,
+                    unsigned long long *__restrict__ partials, uint32_t *__restrict__ counters,
+                    const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
+                    const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_x4k,
+                    uint64_t S, uint32_t W, uint32_t n, uint32_t ntiny,
+                    unsigned long long *stamps = nullptr)
+{
+    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+    const uint32_t tid = threadIdx.x;
+    unsigned long long t_entry = 0, t_tables = 0, t_stream = 0;
+    if (STAMPS) {
+        t_entry = __builtin_amdgcn_s_memrealtime();
+    }
+
+    // Table words first: vmcnt is in order, so loads issued after them (the
+    // ring prologue) do not delay the table build.
+    const uint32_t tab_v = g_slice[tid];
+    const uint32_t tab_sv = g_shift[tid];
+
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (tid >> 6));
+    const uint32_t lane = tid & 63u;
+    const uint32_t lb_lo = (lane & 31u) << 2;
+    const uint32_t lb_hi = lb_lo | 0x10000u;
+    const uint32_t lrep = (lane & 7u) << 2;
+    const uint32_t slot_group = __builtin_amdgcn_readfirstlane((tid >> 6) >> 2);
+    const uint64_t g0 = wave_start(wave, S, W);
+    const uint64_t gend = wave_start((uint64_t) wave + 1, S, W);
+    const bool active = g0 < gend;
+
+    // Compute cursor (c, d, j) and load cursor (lc, ld, lj) walk the same
+    // step sequence; the load cursor runs D steps ahead.
+    uint32_t c = 0, lc = 0;
+    ChunkDesc d = {}, ld = {};
+    uint64_t j = 0, lj = 0, nload = 0;
+    if (active) {
+        c = wave_chunk0[wave];
+        d = desc[c];
+        j = g0 - d.g;
+        lc = c;
+        ld = d;
+        lj = j;
+        nload = gend - g0;
+    }
+
+    // Waves without steps (only when the batch has fewer steps than waves)
+    // point their loads at the always-valid 4 KiB slice table.
+    const uint8_t *lbase = active ? base : reinterpret_cast<const uint8_t *>(g_slice);
+    if (!active) {
+        ld.a = 0;
+        ld.vlen = kGran;
+        ld.nsteps = 1;
+    }
+
+    auto issue = [&](StepRegs &r) {
+        // Past the wave's range the last step is re-read (cache-resident) so
+        // that every refill is the same 4 loads.
+        const uint64_t jj = nload > 0 ? lj : (uint64_t) ld.nsteps - 1;
+        load_step(r, lbase + ld.a, jj, ld.vlen, lane);
+        if (nload > 0) {
+            --nload;
+            if (++lj == ld.nsteps && nload > 0) {
+                do {
+                    ++lc;
+                    ld = desc[lc];
+                } while (ld.nsteps == 0);
+                lj = 0;
+            }
+        }
+    };
+
+    // The first D steps are requested before the table build so that their
+    // HBM latency overlaps it.
+    // Unconditional (also for inactive waves): a branch here would merge a
+    // no-load path into the vmcnt state and make the table build wait for the ring.
+    StepRegs ring[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        issue(ring[k]);
+    }
+
+    {   // Tables: thread tid owns entry b of table k (tid = 256 k + b).
+        const uint32_t k = tid >> 8, b = tid & 255u;
+        const uint32_t v = tab_v;
+        const uint4 v4 = make_uint4(v, v, v, v);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds + ((k >> 1) << 16) + (b << 8) + ((k & 1u) << 7));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            dst[q] = v4;
+        }
+        const uint32_t sv = tab_sv;
+        uint4 *sd = reinterpret_cast<uint4 *>(lds + kShiftOff + k * 8192u + b * 32u);
+        sd[0] = make_uint4(sv, sv, sv, sv);
+        sd[1] = make_uint4(sv, sv, sv, sv);
+    }
+    __syncthreads();
+    if (STAMPS) {
+        t_tables = __builtin_amdgcn_s_memrealtime();
+    }
+
+    if (active) {
+        uint32_t s[kSub] = {0u, 0u, 0u, 0u};
+        uint64_t e[kSub] = {0ull, 0ull, 0ull, 0ull};
+        uint64_t full_end = d.vlen / kStep;
+        uint32_t seed = (j == 0) ? (seeds ? seeds[cid ? cid[c] : c] : 0xffffffffu) : 0u;
+        uint64_t g = g0;
+
+        // One step: CRC the ring slot (if the wave's range is not exhausted),
+        // publish a piece at a chunk / range end, then refill the slot.
+        auto body = [&](StepRegs &r) {
+            if (g < gend) {
+                if (j != 0 && j < full_end) {
+#pragma unroll
+                    for (int q = 0; q < kSub; ++q) {
+                        s[q] = block16(lds, lb_lo, lb_hi, step_shift(lds, lrep, s[q]), r.q[q]);
+                    }
+                    const uint64_t e0 = j * kStep + (uint64_t) (lane + 1) * kGran;
+#pragma unroll
+                    for (int q = 0; q < kSub; ++q) {
+                        e[q] = e0 + (uint64_t) q * kRow;
+                    }
+                } else {
+                    slow_compute(lds, lb_lo, lb_hi, lrep, r, j, d.vlen, d.h, seed, lane, s, e);
+                }
+                ++g;
+                ++j;
+                if (j == d.nsteps || g == gend) {
+                    // Piece end: shift every sub-chain state to the piece end,
+                    // reduce over the wave, publish (write-through, agent scope).
+                    const uint64_t pend = min(j * kStep, d.vlen);
+                    uint32_t contrib = 0;
+#pragma unroll
+                    for (int q = 0; q < kSub; ++q) {
+                        const uint64_t dist = e[q] < pend ? pend - e[q] : 0;
+                        contrib ^= s[q] ? multmodp(g_x8[min(dist, (uint64_t) (kX8Count - 1))], s[q]) : 0u;
+                    }
+                    contrib = wave_xor(contrib);
+                    __hip_atomic_store(&partials[(uint64_t) wave + c], (unsigned long long) contrib,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (g < gend) {
+                        do {
+                            ++c;
+                            d = desc[c];
+                        } while (d.nsteps == 0);
+                        j = 0;
+#pragma unroll
+                        for (int q = 0; q < kSub; ++q) {
+                            s[q] = 0u;
+                            e[q] = 0ull;
+                        }
+                        full_end = d.vlen / kStep;
+                        seed = seeds ? seeds[cid ? cid[c] : c] : 0xffffffffu;
+                    }
+                }
+            }
+            issue(r);
+        };
+
+        // Fixed trip count and a single latch: the loop back edge carries only
+        // the state in which every ring slot was refilled, so the compiler waits
+        // for a slot with vmcnt(4 * (D - 1)) instead of draining the ring.
+        static_assert(D >= 1 && D <= 4, "ring depth");
+        const uint64_t iters = (gend - g0 + D - 1) / D;
+        for (uint64_t it = 0; it < iters; ++it) {
+            if (PRIO) {
+                rotate_prio(slot_group, it);
+            }
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                body(ring[k]);
+            }
+        }
+        if (PRIO) {
+            __builtin_amdgcn_s_setprio(0);
+        }
+
+        // Arrive on every chunk this wave published a piece of; the last
+        // arriver folds the chunk.  The partial stores above are write-through
+        // (agent scope); drain them before counting.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (STAMPS) {
+            t_stream = __builtin_amdgcn_s_memrealtime();
+        }
+        uint32_t ac = wave_chunk0[wave];
+        for (;;) {
+            const ChunkDesc ad = desc[ac];
+            if (ad.nsteps != 0) {
+                if (ad.g >= gend) {
+                    break;
+                }
+                uint32_t old = 0;
+                if (lane == 0) {
+                    old = __hip_atomic_fetch_add(&counters[ac], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                }
+                old = __shfl(old, 0);
+                if (old + 1 == ad.npieces) {
+                    fold_chunk(ad, ac, cid ? cid[ac] : ac, lane, partials, out, counters, g_x8, g_x4k,
+                               S, W);
+                }
+            }
+            if (++ac >= n) {
+                break;
+            }
+        }
+    }
+
+    // Tiny chunks (len < 4) and empty chunks: byte-serial with the seed.
+    for (uint64_t t = (uint64_t) wave * kWave + lane; t < ntiny; t += (uint64_t) W * kWave) {
+        const uint32_t c = tiny[t];
+        const ChunkDesc d = desc[c];
+        const uint32_t oc = cid ? cid[c] : c;
+        uint32_t st = seeds ? seeds[oc] : 0xffffffffu;
         const uint8_t *p = base + d.a + d.h;
         const uint32_t len = (uint32_t) (d.vlen - d.h);
         for (uint32_t i = 0; i < len; ++i) {
-            s = g_byte[(s ^ p[i]) & 0xffu] ^ (s >> 8);
+            st = byte_step(lds, lb_lo, st, p[i]);
         }
-        out[oc] = s;
-        return;
+        out[oc] = st;
     }
-    const uint64_t w0 = wave_of_step(d.g, S, W);
-    const uint64_t w1 = wave_of_step(d.g + d.nsteps - 1, S, W);
-    uint32_t acc = partials[w0 + c];
-    for (uint64_t w = w0 + 1; w <= w1; ++w) {
-        const uint64_t st = wave_start(w, S, W);
-        const uint64_t en = wave_start(w + 1, S, W);
-        if (st == en) {
-            continue;   // empty wave (S < W)
-        }
-        const uint64_t ps = st - d.g;
-        const uint64_t pe = min(en - d.g, (uint64_t) d.nsteps);
-        const uint64_t bytes = (w == w1) ? d.vlen - ps * kStep : (pe - ps) * kStep;
-        acc = multmodp(xpow8_bytes(bytes, g_x8, g_x4k), acc) ^ partials[w + c];
+    if (STAMPS && lane == 0) {
+        // Diagnostic build only: 100 MHz global clock, per wave.
+        stamps[4 * wave + 0] = t_entry;
+        stamps[4 * wave + 1] = t_tables;
+        stamps[4 * wave + 2] = t_stream;
+        stamps[4 * wave + 3] = __builtin_amdgcn_s_memrealtime();
     }
-    out[oc] = acc;
 }
 
 // ---------------------------------------------------------------- synthetic fill
@@ -454,7 +639,7 @@ int device_state(DeviceState **out)
         static uint32_t slice[4][256], shift[4][256];
         std::vector<uint32_t> x8(kX8Count);
         cioa_gen_slice4(slice);
-        cioa_gen_shift_table(shift, (uint64_t) (kStep - kBPL));
+        cioa_gen_shift_table(shift, (uint64_t) (kStep - kGran));
         cioa_gen_xpow8_table(x8.data(), kX8Count, 1);
         HIP_TRY(hipMalloc(&st.slice, sizeof(slice)), "hipMalloc(slice)");
         HIP_TRY(hipMalloc(&st.shift, sizeof(shift)), "hipMalloc(shift)");
@@ -471,16 +656,23 @@ int device_state(DeviceState **out)
 
 }  // namespace
 
+constexpr int kRingDefault = 1;   // steps in flight per wave beyond the one computing (tools/sweep.py: 1 is fastest)
+
 struct cio_crc32_plan {
-    int device = 0;
     uint32_t n = 0;
     uint64_t S = 0;            // total wave-steps
     uint32_t W = 0;            // waves in the grid
     uint32_t grid = 0;         // workgroups
+    uint32_t ntiny = 0;        // chunks with len < 4 (byte-serial)
+    int ring = kRingDefault;   // CIO_GPU_RING=1..4 overrides (tuning)
+    int prio = 1;              // CIO_GPU_PRIO=0 disables the priority rotation
+    unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     ChunkDesc *desc = nullptr;
     uint32_t *wave_chunk0 = nullptr;
-    uint32_t *partials = nullptr;
+    uint32_t *tiny = nullptr;
+    unsigned long long *partials = nullptr;
+    uint32_t *counters = nullptr;
     uint32_t *x4k = nullptr;
     DeviceState *st = nullptr;
 };
@@ -494,7 +686,7 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v1 gfx950 lane64B-step4K slice4-lds32x";
+    return "chunkio_amd crc32 v3 gfx950 fused-stream ring1 prio-rotate coalesced-nt 4x16B-subchains slice4-lds32x perm";
 }
 
 int cio_gpu_init(void)
@@ -510,8 +702,11 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
     }
     (void) hipFree(p->desc);
     (void) hipFree(p->wave_chunk0);
+    (void) hipFree(p->tiny);
     (void) hipFree(p->partials);
+    (void) hipFree(p->counters);
     (void) hipFree(p->x4k);
+    (void) hipFree(p->stamps);
     delete p;
 }
 
@@ -531,13 +726,29 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     cio_crc32_plan *p = new cio_crc32_plan();
     p->st = st;
     p->n = (uint32_t) n;
+    if (const char *r = getenv("CIO_GPU_PRIO")) {
+        p->prio = atoi(r) ? 1 : 0;
+    }
+    if (const char *r = getenv("CIO_GPU_RING")) {
+        const int v = atoi(r);
+        if (v >= 1 && v <= 4) {
+            p->ring = v;
+        }
+    }
     p->grid = (uint32_t) st->cus;
     p->W = p->grid * kWavesPerWG;
+    if (const char *r = getenv("CIO_GPU_STAMPS")) {
+        if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * 4 * sizeof(unsigned long long)) != hipSuccess) {
+            p->stamps = nullptr;
+        }
+    }
 
     std::vector<ChunkDesc> desc(n ? n : 1);
+    std::vector<uint32_t> tiny;
     uint64_t S = 0, bytes = 0, max_steps = 0;
     for (size_t i = 0; i < n; i++) {
         ChunkDesc &d = desc[i];
+        memset(&d, 0, sizeof(d));
         d.a = offs[i] & ~15ull;
         d.h = (uint32_t) (offs[i] & 15u);
         d.vlen = d.h + lens[i];
@@ -548,43 +759,76 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
             return fail("cio_crc32_plan_create: chunk too large");
         }
         d.nsteps = (uint32_t) ns;
+        if (ns == 0) {
+            tiny.push_back((uint32_t) i);
+        }
         S += ns;
         bytes += lens[i];
         max_steps = std::max(max_steps, ns);
     }
     p->S = S;
     p->bytes = bytes;
+    p->ntiny = (uint32_t) tiny.size();
 
-    // First non-empty chunk of every wave's step range.
+    // First non-empty chunk of every wave's step range, and per chunk the
+    // number of (non-empty) waves that hold a piece of it.
     std::vector<uint32_t> wc(p->W, 0);
-    {
+    if (S > 0) {
         size_t c = 0;
         for (uint32_t w = 0; w < p->W; w++) {
-            const uint64_t g0 = (S == 0) ? 0 : ((uint64_t) w * S) / p->W;
+            const uint64_t g0 = ((uint64_t) w * S) / p->W;
+            const uint64_t g1 = ((uint64_t) (w + 1) * S) / p->W;
             while (c < n && (desc[c].nsteps == 0 || desc[c].g + desc[c].nsteps <= g0)) {
                 c++;
             }
-            wc[w] = (uint32_t) std::min(c, n ? n - 1 : 0);
+            wc[w] = (uint32_t) std::min(c, n - 1);
+            if (g0 == g1) {
+                continue;
+            }
+            for (size_t k = c; k < n && desc[k].g < g1; k++) {
+                if (desc[k].nsteps) {
+                    desc[k].npieces++;
+                }
+            }
         }
     }
-    const uint64_t per_wave = S / p->W + 2;
-    const uint64_t nx4k = std::min(max_steps, per_wave) + 2;
+    const uint64_t nx4k = max_steps + 2;
     std::vector<uint32_t> x4k(nx4k);
     cioa_gen_xpow8_table(x4k.data(), nx4k, (uint64_t) kStep);
 
     hipError_t e;
+    const size_t npart = (size_t) p->W + n + 1;
     if ((e = hipMalloc(&p->desc, desc.size() * sizeof(ChunkDesc))) != hipSuccess ||
         (e = hipMalloc(&p->wave_chunk0, wc.size() * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMalloc(&p->partials, ((size_t) p->W + n + 1) * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(&p->tiny, std::max<size_t>(1, tiny.size()) * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(&p->partials, npart * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc(&p->counters, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&p->x4k, nx4k * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemcpy(p->desc, desc.data(), desc.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->wave_chunk0, wc.data(), wc.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess ||
+        (tiny.size() && (e = hipMemcpy(p->tiny, tiny.data(), tiny.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) ||
+        (e = hipMemset(p->partials, 0, npart * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMemset(p->counters, 0, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemcpy(p->x4k, x4k.data(), nx4k * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) {
         cio_crc32_plan_destroy(p);
         return fail("cio_crc32_plan_create: device allocation/upload", e);
     }
     *out = p;
     return CIO_OK;
+}
+
+/* Diagnostic (not in the public header): copy the per-wave timestamps of the
+ * last launch of a CIO_GPU_STAMPS=1 plan; returns the number of waves. */
+int cioa_debug_stamps(const cio_crc32_plan *p, unsigned long long *host, size_t cap)
+{
+    if (!p || !p->stamps) {
+        return 0;
+    }
+    const size_t n = std::min(cap, (size_t) p->W * 4);
+    if (hipMemcpy(host, p->stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) {
+        return 0;
+    }
+    return (int) p->W;
 }
 
 uint64_t cio_crc32_plan_bytes(const cio_crc32_plan *p)
@@ -615,6 +859,9 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 }  // extern "C"
 
+// One launch: stream kernel (CRC of every step, per-chunk fold by the last
+// arriver, tiny chunks).  The per-chunk counters are self-resetting, so no
+// memset node precedes it and the launch can be captured in a HIP graph.
 static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const uint32_t *dev_seeds,
                           uint32_t *dev_out, const uint32_t *cid, hipStream_t s,
                           hipEvent_t ev0, hipEvent_t ev1)
@@ -632,20 +879,33 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
-    if (p->S > 0) {
-        hipLaunchKernelGGL(crc32_piece_kernel, dim3(p->grid), dim3(kThreads), 0, s,
-                           reinterpret_cast<const uint8_t *>(dev_base), p->desc, p->wave_chunk0,
-                           dev_seeds, p->partials, st->slice, st->shift, st->x8, cid, p->S, p->W, p->n);
-        HIP_TRY(hipGetLastError(), "crc32_piece_kernel launch");
+    auto kern = crc32_stream_kernel<kRingDefault, false, 1>;
+    if (p->prio) {
+        switch (p->ring) {
+        case 1: kern = crc32_stream_kernel<1, false, 1>; break;
+        case 2: kern = crc32_stream_kernel<2, false, 1>; break;
+        case 4: kern = crc32_stream_kernel<4, false, 1>; break;
+        default: break;
+        }
+    } else {
+        switch (p->ring) {
+        case 1: kern = crc32_stream_kernel<1, false, 0>; break;
+        case 2: kern = crc32_stream_kernel<2, false, 0>; break;
+        case 4: kern = crc32_stream_kernel<4, false, 0>; break;
+        default: kern = crc32_stream_kernel<kRingDefault, false, 0>; break;
+        }
     }
+    if (p->stamps) {
+        kern = p->prio ? crc32_stream_kernel<kRingDefault, true, 1> : crc32_stream_kernel<kRingDefault, true, 0>;
+    }
+    hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
+                       reinterpret_cast<const uint8_t *>(dev_base), p->desc, p->wave_chunk0, p->tiny,
+                       dev_seeds, dev_out, cid, p->partials, p->counters, st->slice, st->shift,
+                       st->x8, p->x4k, p->S, p->W, p->n, p->ntiny, p->stamps);
+    HIP_TRY(hipGetLastError(), "crc32_stream_kernel launch");
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");
     }
-    const uint32_t fb = 256;
-    hipLaunchKernelGGL(crc32_finish_kernel, dim3((p->n + fb - 1) / fb), dim3(fb), 0, s,
-                       reinterpret_cast<const uint8_t *>(dev_base), p->desc, dev_seeds,
-                       p->partials, dev_out, st->slice, st->x8, p->x4k, cid, p->S, p->W, p->n);
-    HIP_TRY(hipGetLastError(), "crc32_finish_kernel launch");
     return CIO_OK;
 }
 

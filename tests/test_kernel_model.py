@@ -2,8 +2,9 @@
 
 Re-plays, in Python, exactly the work split of crc32_gpu.hip -- plan
 construction (virtual aligned chunks, wave-steps, even split over W waves,
-first chunk per wave), per-lane 64-byte blocks with the 4032-byte step shift,
-head zeroing + seed fold, partial last steps, per-lane shift to the piece end,
+first chunk per wave), per-(sub-chain, lane) 16-byte blocks [1024 q + 16 lane, +16) with the
+4080-byte step shift, head zeroing + seed fold (which can straddle lanes 0 and
+1), partial last steps, per-sub-chain shift to the piece end,
 piece slots (wave + chunk) and the finisher's Horner fold -- using the oracle
 for the per-lane byte CRCs and GF(2) shifts.  Any index slip in that scheme
 shows up here as a CRC mismatch against crc_update on the whole chunk.
@@ -13,7 +14,8 @@ import pytest
 
 from oracle import pyoracle as po
 
-STEP, BPL, WAVE = 4096, 64, 64
+STEP, GRAN, SUB, WAVE = 4096, 16, 4, 64
+ROW = GRAN * WAVE
 INIT = 0xFFFFFFFF
 
 
@@ -34,15 +36,19 @@ def plan(offs, lens, W):
     return desc, S, wc
 
 
-def lane_block(buf, d, jj, lane, seed):
-    """Bytes of lane `lane` at step jj (virtual chunk, head zeroed, seed folded)."""
-    bstart = jj * STEP + lane * BPL
-    vb = 0 if bstart >= d["vlen"] else min(d["vlen"] - bstart, BPL)
+def lane_block(buf, d, jj, q, lane, seed):
+    """Bytes of (sub-chain q, lane) at step jj (virtual chunk, head zeroed, seed folded)."""
+    bstart = jj * STEP + q * ROW + lane * GRAN
+    vb = 0 if bstart >= d["vlen"] else min(d["vlen"] - bstart, GRAN)
     blk = np.array(buf[d["a"] + bstart: d["a"] + bstart + vb], dtype=np.uint8)
-    if jj == 0 and lane == 0 and vb:
-        blk[:d["h"]] = 0
+    if jj == 0 and q == 0 and vb:
         sb = np.frombuffer(int(seed).to_bytes(4, "little"), np.uint8)
-        blk[d["h"]:d["h"] + 4] ^= sb
+        for k in range(vb):
+            pos = bstart + k                      # virtual position
+            if pos < d["h"]:
+                blk[k] = 0
+            elif pos < d["h"] + 4:
+                blk[k] ^= sb[pos - d["h"]]
     return bstart, vb, blk
 
 
@@ -59,23 +65,24 @@ def model(buf, offs, lens, seeds, W):
         j = g - d["g"]
         while True:
             jend = min(d["nsteps"], j + (gend - g))
-            s = [0] * WAVE
-            lane_end = [0] * WAVE
+            s = {}
+            end = {}
             for jj in range(j, jend):
-                for lane in range(WAVE):
-                    bstart, vb, blk = lane_block(buf, d, jj, lane, seeds[c] if jj == 0 else 0)
-                    if vb == 0:
-                        continue
-                    st = po.crc_shift(s[lane], STEP - BPL)     # step shift (any state)
-                    s[lane] = po.crc_update(st, blk)
-                    lane_end[lane] = bstart + vb
+                for q in range(SUB):
+                    for lane in range(WAVE):
+                        bstart, vb, blk = lane_block(buf, d, jj, q, lane, seeds[c] if jj == 0 else 0)
+                        if vb == 0:
+                            continue
+                        st = po.crc_shift(s.get((q, lane), 0), STEP - GRAN)   # step shift
+                        s[(q, lane)] = po.crc_update(st, blk)
+                        end[(q, lane)] = bstart + vb
             pend = min(jend * STEP, d["vlen"])
             acc = 0
-            for lane in range(WAVE):
-                if s[lane]:
-                    dist = max(0, pend - lane_end[lane])
+            for key, st in s.items():
+                if st:
+                    dist = max(0, pend - end[key])
                     assert dist < 2 * STEP
-                    acc ^= po.crc_shift(s[lane], dist)
+                    acc ^= po.crc_shift(st, dist)
             slot = w + c
             assert slot not in partials
             partials[slot] = acc

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Per-wave phase timestamps of the CRC kernel (diagnostic build, CIO_GPU_STAMPS=1)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    os.environ["CIO_GPU_STAMPS"] = "1"
+    import torch
+    import chunkio_amd as cio
+    from chunkio_amd import workloads as wl
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
+    lens = wl.cfg2_lens() if cfg == "cfg2" else np.full(1024, 4 << 20, np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    dev = torch.device("cuda:0")
+    buf = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=dev)
+    cio.fill_synthetic(buf, offs, lens, 1)
+    out = torch.empty(len(lens), dtype=torch.int32, device=dev)
+    plan = cio.Crc32Plan(offs, lens)
+    f = cio.lib().cioa_debug_stamps
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
+    for it in range(5):
+        plan.exec(buf, out)
+        torch.cuda.synchronize()
+        st = np.zeros(4096 * 4 * 2, np.uint64)
+        W = f(plan._handle, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), st.size)
+        t = st[:W * 4].reshape(W, 4).astype(np.int64)
+        t0 = t[:, 0].min()
+        us = (t - t0) / 100.0     # 100 MHz
+        q = lambda a: " ".join(f"{np.percentile(a, p):7.2f}" for p in (0, 10, 50, 90, 100))  # noqa: E731
+        print(f"{cfg} iter {it}: span {us[:, 3].max():7.2f} us   [pct 0/10/50/90/100]")
+        print("   entry      ", q(us[:, 0]))
+        print("   tables done", q(us[:, 1]))
+        print("   stream done", q(us[:, 2]))
+        print("   exit       ", q(us[:, 3]))
+        print("   stream dur ", q(us[:, 2] - us[:, 1]))
+        print("   tail dur   ", q(us[:, 3] - us[:, 2]))
+        wg = us[:, 2].reshape(-1, 16)
+        print("   WG max done", q(wg.max(1)))
+        print("   WG min done", q(wg.min(1)))
+        print("   WG spread  ", q(wg.max(1) - wg.min(1)))
+        # rank of wave within its WG (by finish) vs wave index in WG
+        order = np.argsort(wg, axis=1)
+        print("   mean finish by wave slot", " ".join(f"{x:5.1f}" for x in wg.mean(0)))
+        xcd = np.arange(wg.shape[0]) % 8
+        print("   WG max by blockIdx%8   ", " ".join(f"{wg.max(1)[xcd == k].mean():6.1f}" for k in range(8)))
+
+
+if __name__ == "__main__":
+    main()
