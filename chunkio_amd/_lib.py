@@ -22,6 +22,8 @@ EXPORTS = (
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
+    # include/chunkio_amd/cio_verify.h
+    "cio_file_verify_batch", "cio_verify_paths",
 )
 
 _lib = None

@@ -1,0 +1,284 @@
+"""Chunk-file layer: the reference's on-disk format and CRC lifecycle, host side.
+
+Mirrors fluent/chunkio's filesystem backend for one chunk (names follow the
+reference's functions; file:line citations into /root/reference):
+
+  ChunkFile.open(path, flags)     cio_file_open + mmap_file + cio_file_format_check
+                                  (src/cio_file.c:636-782, 345-493, 187-294)
+  ChunkFile.write(data)           cio_file_write (src/cio_file.c:994-1073):
+                                  grow in realloc_size steps (8 pages,
+                                  include/chunkio/chunkio.h:59-66), update_checksum
+                                  (:97-113, raw 8-byte state at map+2), copy, BE length
+  ChunkFile.write_at(data, off)   cio_chunk_write_at (src/cio_chunk.c:184-209): truncate
+                                  + crc_reset -> full recompute on the next write
+  ChunkFile.write_metadata(meta)  cio_file_write_metadata + adjust_layout (:1075-1145, 130-146)
+  ChunkFile.sync()                cio_file_sync (:1147-1250): finalize_checksum (:116-124)
+  ChunkFile.hash()                cio_file_hash (:1304-1307): the 4 bytes at map+2
+  ChunkFile.down()/up()           munmap_file / _cio_file_up (re-verify on map)
+
+Every CRC of a whole region (verify on open/up, metadata recompute) goes
+through the batched GPU path (cio_file_verify_batch / cio_crc32_batch_host);
+the incremental per-write update uses crc_update on the caller's buffer, as
+the reference does at src/cio_file.c:110.
+
+verify_paths(paths) is the batched verify-on-load of a stream directory
+(cio_scan_stream_files, src/cio_scan.c:39-125) in one GPU pass.
+"""
+import ctypes
+import mmap
+import os
+import struct
+
+import numpy as np
+
+from . import _lib
+from .crc32 import crc_update
+
+CIO_OK, CIO_ERROR, CIO_RETRY, CIO_CORRUPTED = 0, -1, -2, -3
+CIO_OPEN, CIO_OPEN_RD, CIO_CHECKSUM = 1, 2, 4
+CIO_ERR_BAD_CHECKSUM, CIO_ERR_BAD_LAYOUT, CIO_ERR_PERMISSION, CIO_ERR_BAD_FILE_SIZE = -10, -11, -12, -13
+CIOA_VERIFY_WRITEBACK = 64
+
+HDR_MIN = 24
+CONTENT_OFFSET = 22
+CONTENT_LEN_OFFSET = 10
+# cio_file_init_bytes (src/cio_file.c:45-60): C1 00, CRC32("\0\0") LE, zeros
+INIT_BYTES = bytes([0xC1, 0x00, 0xFF, 0x12, 0xD9, 0x41]) + bytes(18)
+CRC_INIT = 0xFFFFFFFF
+PAGE = mmap.PAGESIZE
+
+
+def _round_up(n, s):
+    return ((n + s - 1) // s) * s
+
+
+class VerifyItem(ctypes.Structure):
+    _fields_ = [("map", ctypes.c_void_p), ("fs_size", ctypes.c_size_t), ("taint", ctypes.c_int),
+                ("status", ctypes.c_int), ("error", ctypes.c_int), ("crc_raw", ctypes.c_uint32),
+                ("meta_len", ctypes.c_uint16), ("content_len", ctypes.c_uint64)]
+
+
+def _bind():
+    lib = _lib.lib()
+    if not hasattr(lib, "_verify_bound"):
+        lib.cio_file_verify_batch.restype = ctypes.c_int
+        lib.cio_file_verify_batch.argtypes = [ctypes.POINTER(VerifyItem), ctypes.c_size_t, ctypes.c_int]
+        lib.cio_verify_paths.restype = ctypes.c_int
+        lib.cio_verify_paths.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_uint32)]
+        lib._verify_bound = True
+    return lib
+
+
+def verify_paths(paths, flags=CIO_CHECKSUM):
+    """Batched verify-on-load: (status, error, crc_raw) numpy arrays per path."""
+    lib = _bind()
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    st = np.zeros(max(n, 1), np.int32)
+    er = np.zeros(max(n, 1), np.int32)
+    cr = np.zeros(max(n, 1), np.uint32)
+    rc = lib.cio_verify_paths(arr, n, flags, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                              er.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                              cr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    _lib.check(rc, "cio_verify_paths")
+    return st[:n], er[:n], cr[:n]
+
+
+class ChunkFile:
+    """One filesystem chunk with the reference's layout and CRC semantics."""
+
+    def __init__(self, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None):
+        self.path = path
+        self.flags = flags
+        self.realloc_size = realloc_size or PAGE * 8
+        self.fd = -1
+        self.map = None
+        self.alloc_size = 0
+        self.fs_size = 0
+        self.data_size = 0
+        self.crc_cur = CRC_INIT
+        self.crc_reset = False
+        self.taint = False
+        self.synced = True
+        self.error = 0
+
+    # -- open / map -------------------------------------------------------
+    @classmethod
+    def open(cls, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None):
+        cf = cls(path, flags, realloc_size)
+        rc = cf.up()
+        if rc != CIO_OK:
+            cf._close_fd()
+        return cf, rc
+
+    def up(self):
+        """Open + map + format check (src/cio_file.c:345-493, 187-294)."""
+        if self.map is not None:
+            return CIO_OK
+        rw = bool(self.flags & CIO_OPEN)
+        self.fd = os.open(self.path, (os.O_RDWR | os.O_CREAT) if rw else os.O_RDONLY, 0o600)
+        fs_size = os.fstat(self.fd).st_size
+        self.taint = False
+        if fs_size == 0:
+            if not rw:
+                self.error = CIO_ERR_PERMISSION
+                return CIO_CORRUPTED
+            size = _round_up(HDR_MIN, PAGE)
+            os.posix_fallocate(self.fd, 0, size)
+            self.alloc_size = size
+            self.map = mmap.mmap(self.fd, size)
+            self.map[:HDR_MIN] = INIT_BYTES
+            if not (self.flags & CIO_CHECKSUM):
+                self.map[2:6] = bytes(4)
+            self._set_content_len(0)
+            self.data_size = 0
+            self.fs_size = 0
+            self.synced = False
+            if self.flags & CIO_CHECKSUM:
+                self.crc_cur = crc_update(CRC_INIT, self.map[CONTENT_OFFSET:CONTENT_OFFSET + 2])
+            return CIO_OK
+        prot = mmap.PROT_READ | (mmap.PROT_WRITE if rw else 0)
+        self.map = mmap.mmap(self.fd, fs_size, prot=prot)
+        self.alloc_size = fs_size
+        self.fs_size = fs_size
+        self.synced = True
+        # header checks + (batched, GPU) CRC verify of this one chunk
+        item = (VerifyItem * 1)()
+        if rw:
+            view = (ctypes.c_char * fs_size).from_buffer(self.map)
+            addr = ctypes.addressof(view)
+        else:
+            view = np.frombuffer(self.map, dtype=np.uint8)
+            addr = view.ctypes.data
+        item[0].map = addr
+        item[0].fs_size = fs_size
+        item[0].taint = 0
+        vflags = (self.flags & CIO_CHECKSUM) | (CIOA_VERIFY_WRITEBACK if rw else 0)
+        _lib.check(_bind().cio_file_verify_batch(item, 1, vflags), "cio_file_verify_batch")
+        del view
+        self.error = item[0].error
+        if item[0].status != CIO_OK:
+            # cio_file_format_check failure: map released, fd closed (tests/fs.c:719-722)
+            self.map.close()
+            self.map = None
+            self._close_fd()
+            return CIO_CORRUPTED
+        self.data_size = int(item[0].content_len)
+        if self.flags & CIO_CHECKSUM:
+            self.crc_cur = int(item[0].crc_raw)
+        return CIO_OK
+
+    def down(self):
+        if self.map is None:
+            return CIO_ERROR
+        if not self.synced:
+            self.sync()
+        self.map.close()
+        self.map = None
+        self._close_fd()
+        return CIO_OK
+
+    def close(self):
+        if self.map is not None:
+            self.down()
+        self._close_fd()
+
+    def _close_fd(self):
+        if self.fd >= 0:
+            os.close(self.fd)
+            self.fd = -1
+
+    # -- layout helpers (include/chunkio/cio_file_st.h) -----------------------
+    def meta_len(self):
+        return (self.map[CONTENT_OFFSET] << 8) | self.map[CONTENT_OFFSET + 1]
+
+    def _set_content_len(self, n):
+        self.map[CONTENT_LEN_OFFSET:CONTENT_LEN_OFFSET + 4] = struct.pack(">I", n)
+
+    def content(self):
+        off = HDR_MIN + self.meta_len()
+        return bytes(self.map[off:off + self.data_size])
+
+    def hash(self):
+        return bytes(self.map[2:6])
+
+    def _region_crc(self):
+        """crc_update(init, map+22, 2 + meta + data) -- cio_file_calculate_checksum."""
+        from .crc32 import crc32_batch_host
+        n = 2 + self.meta_len() + self.data_size
+        view = np.frombuffer(self.map, dtype=np.uint8)[CONTENT_OFFSET:CONTENT_OFFSET + n]
+        return int(crc32_batch_host([view])[0])
+
+    # -- writes ---------------------------------------------------------------
+    def _resize(self, new_size):
+        os.posix_fallocate(self.fd, 0, new_size)
+        self.map.resize(new_size)
+        self.alloc_size = new_size
+        self.fs_size = new_size
+
+    def write(self, data):
+        """cio_file_write (src/cio_file.c:994-1073)."""
+        data = bytes(data)
+        if not data:
+            return 0
+        if self.map is None:
+            return -1
+        meta = self.meta_len()
+        av = self.alloc_size - HDR_MIN - meta - self.data_size
+        if av < len(data):
+            pre = HDR_MIN + meta
+            new_size = self.alloc_size + self.realloc_size
+            while new_size < pre + self.data_size + len(data):
+                new_size += self.realloc_size
+            self._resize(_round_up(new_size, PAGE))
+        if self.crc_reset:
+            self._set_content_len(self.data_size)
+        if self.flags & CIO_CHECKSUM:
+            if self.crc_reset:                       # update_checksum (:103-108)
+                self.crc_cur = self._region_crc()
+                self.crc_reset = False
+            self.crc_cur = crc_update(self.crc_cur, data)
+            self.map[2:10] = struct.pack("<Q", self.crc_cur)   # raw 8-byte crc_t (:111)
+        off = HDR_MIN + meta + self.data_size
+        self.map[off:off + len(data)] = data
+        self.data_size += len(data)
+        self.synced = False
+        self._set_content_len(self.data_size)
+        self.taint = True
+        return 0
+
+    def write_at(self, data, offset):
+        """cio_chunk_write_at (src/cio_chunk.c:184-209)."""
+        self.data_size = offset
+        self.crc_reset = True
+        return self.write(data)
+
+    def write_metadata(self, meta):
+        """cio_file_write_metadata + adjust_layout (src/cio_file.c:1075-1145, 130-146)."""
+        meta = bytes(meta)
+        cur_meta = self.meta_len()
+        content = bytes(self.map[HDR_MIN + cur_meta:HDR_MIN + cur_meta + self.data_size])
+        need = HDR_MIN + len(meta) + self.data_size
+        if cur_meta < len(meta) and self.alloc_size < need:
+            self._resize(need)
+        self.map[HDR_MIN:HDR_MIN + len(meta)] = meta
+        self.map[HDR_MIN + len(meta):HDR_MIN + len(meta) + self.data_size] = content
+        self.map[CONTENT_OFFSET:CONTENT_OFFSET + 2] = struct.pack(">H", len(meta))
+        if self.flags & CIO_CHECKSUM:
+            self.crc_cur = self._region_crc()
+        self.synced = False
+        return 0
+
+    def sync(self):
+        """cio_file_sync (src/cio_file.c:1147-1250) without trimming."""
+        if self.map is None or self.synced or not (self.flags & CIO_OPEN):
+            return 0
+        if self.flags & CIO_CHECKSUM:
+            fin = (self.crc_cur ^ 0xFFFFFFFF) & 0xFFFFFFFF
+            self.map[2:10] = struct.pack("<Q", int.from_bytes(struct.pack(">I", fin), "little"))
+        self.map.flush()
+        self.synced = True
+        self.fs_size = os.fstat(self.fd).st_size
+        return 0

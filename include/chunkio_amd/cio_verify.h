@@ -1,0 +1,75 @@
+/*
+ * cio_verify.h -- batched verify-on-load of chunkio chunk files on the GPU.
+ *
+ * chunkio verifies a chunk when it maps an existing file: cio_scan_stream_files
+ * (src/cio_scan.c:105) -> cio_chunk_open -> cio_file_open -> mmap_file
+ * (src/cio_file.c:345-493) -> cio_file_format_check (src/cio_file.c:187-294).
+ * One chunk at a time, single-threaded.  cio_file_verify_batch() runs the same
+ * checks over N mapped chunk files and computes all their CRCs in ONE batched
+ * GPU pass (cio_crc32_batch_host), returning per chunk exactly what the
+ * reference would have recorded:
+ *
+ *   magic bytes C1 00                        else CIO_ERR_BAD_LAYOUT     (cio_file.c:230-236)
+ *   content length (BE u32 @10), legacy       else CIO_ERR_BAD_FILE_SIZE  (cio_file_st.h:219-269,
+ *     inference when the field is 0                                       cio_file.c:243-251)
+ *   24 + meta_len + content_len <= fs_size    else CIO_ERR_BAD_FILE_SIZE  (cio_file.c:254-264)
+ *   8-byte memcmp of map+2 against htonl(crc_finalize(crc)) held in an
+ *   8-byte crc_t                              else CIO_ERR_BAD_CHECKSUM   (cio_file.c:266-290)
+ *
+ * status is CIO_OK or CIO_CORRUPTED (chunkio.h:50-53); error is one of the
+ * CIO_ERR_* codes (cio_error.h:29-32) or 0.  On success crc_raw is the
+ * un-finalized CRC the reference keeps in cf->crc_cur for later appends.
+ */
+#ifndef CIO_VERIFY_H
+#define CIO_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef CIO_CORRUPTED
+#define CIO_CORRUPTED          -3
+#endif
+#ifndef CIO_ERR_BAD_CHECKSUM
+#define CIO_ERR_BAD_CHECKSUM  -10
+#define CIO_ERR_BAD_LAYOUT    -11
+#define CIO_ERR_PERMISSION    -12
+#define CIO_ERR_BAD_FILE_SIZE -13
+#endif
+
+/* flags */
+#define CIOA_VERIFY_CHECKSUM   4   /* same value as CIO_CHECKSUM (chunkio.h:44) */
+#define CIOA_VERIFY_WRITEBACK  64  /* write an inferred legacy content length back
+                                      into the (writable) map, as chunkio does */
+
+typedef struct cio_verify_item {
+    /* inputs */
+    unsigned char *map;     /* mapped chunk file, fs_size bytes readable */
+    size_t fs_size;         /* file size (fstat) */
+    int taint;              /* cf->taint_flag; 0 for a freshly opened file */
+    /* outputs */
+    int status;             /* CIO_OK or CIO_CORRUPTED */
+    int error;              /* 0 or CIO_ERR_BAD_LAYOUT / _BAD_FILE_SIZE / _BAD_CHECKSUM */
+    uint32_t crc_raw;       /* un-finalized CRC of [map+22, 24+meta_len+content_len) */
+    uint16_t meta_len;
+    uint64_t content_len;   /* cf->data_size */
+} cio_verify_item;
+
+/* Verify n mapped chunk images.  Returns CIO_OK if the batch ran (individual
+ * chunks may still be CIO_CORRUPTED), CIO_ERROR on a GPU/library failure. */
+int cio_file_verify_batch(cio_verify_item *items, size_t n, int flags);
+
+/* Open + mmap (read-only unless CIOA_VERIFY_WRITEBACK) + verify n chunk files,
+ * the batched equivalent of loading a stream directory.  status[i], error[i],
+ * crc_raw[i] per file; a file that cannot be opened/mapped gets CIO_ERROR. */
+int cio_verify_paths(const char *const *paths, size_t n, int flags, int *status,
+                     int *error, uint32_t *crc_raw);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CIO_VERIFY_H */

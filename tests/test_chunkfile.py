@@ -1,0 +1,219 @@
+"""Chunk-file layer vs the reference's own expectations (tests/fs.c,
+tests/metadata_update.c of fluent/chunkio).  The write path (per-write
+crc_update, sync finalisation, file growth) runs on the CPU; every verify
+(open/up of an existing file, batched scan) runs the GPU batch and is marked
+gpu."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from chunkio_amd import chunkfile as cf
+from oracle import pyoracle as po
+
+INIT = 0xFFFFFFFF
+
+
+def hdr_crc_be(path):
+    with open(path, "rb") as f:
+        return struct.unpack(">I", f.read(6)[2:6])[0]
+
+
+def test_new_chunk_header_and_empty_sync(tmp_path, data400):
+    # tests/fs.c:201-206, 254-262: empty chunk after sync -> CRC32("\0\0") = 0x41D912FF
+    p = str(tmp_path / "test1.out")
+    c, rc = cf.ChunkFile.open(p)
+    assert rc == cf.CIO_OK
+    assert c.hash() == bytes([0xFF, 0x12, 0xD9, 0x41])         # init bytes (cio_file.c:49-50)
+    c.sync()
+    assert struct.unpack(">I", c.hash())[0] == 0x41D912FF
+    # tests/fs.c:209-214, 274-282: + 400kb.txt -> 0x103CFA67
+    c.write(data400)
+    assert struct.unpack("<Q", bytes(c.map[2:10]))[0] == po.crc_update(INIT, b"\0\0" + data400)
+    c.sync()
+    assert struct.unpack(">I", c.hash())[0] == 0x103CFA67
+    assert bytes(c.map[6:10]) == bytes(4)                       # 8-byte crc_t: bytes 6..9 zero
+    c.close()
+
+
+def test_cio_perf_file_bytes(tmp_path, data400):
+    # what `tools/cio -k -p 400kb.txt` leaves in each file
+    p = str(tmp_path / "perf-test-0000.txt")
+    c, _ = cf.ChunkFile.open(p)
+    for _ in range(5):
+        c.write(data400)
+    c.sync()
+    c.close()
+    assert os.path.getsize(p) == 2_068_480
+    with open(p, "rb") as f:
+        hdr = f.read(24)
+    assert hdr.hex() == "c100" + "088740e7" + "00000000" + "001f4000" + "00" * 8 + "0000"
+    # the perf-path port in oracle/ writes byte-identical files
+    import ctypes
+    lib = po.oracle()
+    d = tmp_path / "port"
+    d.mkdir()
+    nb = ctypes.c_uint64(0)
+    buf = np.frombuffer(data400, np.uint8)
+    assert lib.oracle_cio_perf_write(str(d).encode(), buf.ctypes.data, buf.size, 1, 5, 1, ctypes.byref(nb)) >= 0
+    assert open(d / "perf-test-0000.txt", "rb").read() == open(p, "rb").read()
+
+
+def test_checksum_off_header(tmp_path):
+    p = str(tmp_path / "nock")
+    c, _ = cf.ChunkFile.open(p, flags=cf.CIO_OPEN)
+    assert c.hash() == bytes(4)                                  # write_init_header (:154-159)
+    c.write(b"hello")
+    c.sync()
+    assert c.hash() == bytes(4)
+    c.close()
+
+
+def test_verify_header_checks_without_crc(tmp_path):
+    """Layout/size checks of cio_file_format_check need no CRC (flags = 0)."""
+    good = tmp_path / "good"
+    c, _ = cf.ChunkFile.open(str(good))
+    c.write(b"x" * 100)
+    c.close()
+    bad_magic = tmp_path / "bad_magic"
+    raw = bytearray(good.read_bytes())
+    raw[0] = 0xC2
+    bad_magic.write_bytes(bytes(raw))
+    short = tmp_path / "short"
+    short.write_bytes(good.read_bytes()[:20])
+    trunc = tmp_path / "trunc"
+    trunc.write_bytes(good.read_bytes()[:24 + 50])              # content_len 100 > file
+    empty = tmp_path / "empty"
+    empty.write_bytes(b"")
+    st, er, crc = cf.verify_paths([str(good), str(bad_magic), str(short), str(trunc), str(empty),
+                                   str(tmp_path / "missing")], flags=0)
+    assert list(st) == [cf.CIO_OK, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_OK,
+                        cf.CIO_ERROR]
+    assert list(er[:4]) == [0, cf.CIO_ERR_BAD_LAYOUT, cf.CIO_ERR_BAD_FILE_SIZE, cf.CIO_ERR_BAD_FILE_SIZE]
+
+
+# ---------------------------------------------------------------- GPU verify
+
+@pytest.mark.gpu
+def test_down_up_keeps_crc(cuda, tmp_path, data400):
+    # tests/fs.c:293-432: CRC survives down/up; up re-verifies the whole region
+    p = str(tmp_path / "updown")
+    c, _ = cf.ChunkFile.open(p)
+    c.write(data400)
+    c.sync()
+    raw = c.crc_cur
+    assert c.down() == cf.CIO_OK
+    assert c.up() == cf.CIO_OK
+    assert c.crc_cur == raw and c.data_size == len(data400)
+    assert struct.unpack(">I", c.hash())[0] == 0x103CFA67
+    c.write(b"more")                                             # append after re-verify
+    c.sync()
+    assert hdr_crc_be(p) == po.crc_update(INIT, b"\0\0" + data400 + b"more") ^ INIT
+    c.close()
+    c2, rc = cf.ChunkFile.open(p)
+    assert rc == cf.CIO_OK
+    assert c2.crc_cur == po.crc_update(INIT, b"\0\0" + data400 + b"more")
+    c2.close()
+
+
+@pytest.mark.gpu
+def test_issue_write_at_and_corruption(cuda, tmp_path):
+    # tests/fs.c:633-724
+    p = str(tmp_path / "test")
+    c, _ = cf.ChunkFile.open(p)
+    line = b"this is a test line\n"
+    for _ in range(3):
+        assert c.write(line) == 0
+    assert c.write_at(b"test\n", len(line) * 2) == 0
+    assert c.down() == cf.CIO_OK
+    assert c.up() == cf.CIO_OK
+    assert c.content() == line * 2 + b"test\n"
+    c.crc_cur = 10                                              # corrupt the running CRC
+    c.write(b"\0")
+    assert c.down() == cf.CIO_OK
+    assert c.up() == cf.CIO_CORRUPTED
+    assert c.error == cf.CIO_ERR_BAD_CHECKSUM
+    assert c.map is None and c.fd < 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("trigger_error", [False, True])
+def test_legacy_content_length(cuda, tmp_path, data400, trigger_error):
+    # tests/fs.c:851-965: zeroed length field, file truncated to 128+24 (ok) / 128+25 (bad)
+    p = str(tmp_path / "test_chunk")
+    c, _ = cf.ChunkFile.open(p)
+    c.write(data400[:128])
+    c.down()
+    with open(p, "r+b") as f:
+        f.seek(10)
+        f.write(bytes(4))
+        f.truncate(128 + 24 + (1 if trigger_error else 0))
+    rc = c.up()
+    if trigger_error:
+        assert rc != cf.CIO_OK
+    else:
+        assert rc == cf.CIO_OK
+        assert c.data_size == 128
+        with open(p, "rb") as f:                                 # inferred length written back
+            assert struct.unpack(">I", f.read(14)[10:14])[0] == 128
+        c.close()
+
+
+@pytest.mark.gpu
+def test_metadata_update_recompute(cuda, tmp_path, data400):
+    # tests/metadata_update.c: metadata moves content, CRC recomputed, verify on reload
+    p = str(tmp_path / "meta")
+    c, _ = cf.ChunkFile.open(p)
+    c.write(data400[:5000])
+    c.write_metadata(b"meta-1")
+    c.write(b"tail")
+    c.write_metadata(b"a-much-longer-metadata-block" * 10)
+    c.sync()
+    c.close()
+    c2, rc = cf.ChunkFile.open(p)
+    assert rc == cf.CIO_OK
+    assert c2.content() == data400[:5000] + b"tail"
+    meta = b"a-much-longer-metadata-block" * 10
+    assert c2.crc_cur == po.crc_update(INIT, struct.pack(">H", len(meta)) + meta + data400[:5000] + b"tail")
+    c2.close()
+
+
+@pytest.mark.gpu
+def test_batched_scan_verify(cuda, tmp_path):
+    rng = np.random.default_rng(31)
+    paths, expect = [], []
+    for i in range(300):
+        p = str(tmp_path / f"chunk-{i:04d}")
+        c, _ = cf.ChunkFile.open(p)
+        if i % 7 == 0:
+            c.write_metadata(bytes(rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8)))
+        for _ in range(int(rng.integers(0, 4))):
+            c.write(bytes(rng.integers(0, 256, int(rng.integers(1, 150000)), dtype=np.uint8)))
+        c.sync()
+        c.close()
+        kind = i % 5
+        raw = bytearray(open(p, "rb").read())
+        clen = struct.unpack(">I", raw[10:14])[0]
+        mlen = struct.unpack(">H", raw[22:24])[0]
+        if kind == 1 and clen > 0:           # flip a content byte
+            raw[24 + mlen + int(rng.integers(0, clen))] ^= 0x40
+            expect.append((cf.CIO_CORRUPTED, cf.CIO_ERR_BAD_CHECKSUM))
+        elif kind == 2:                       # flip a CRC byte
+            raw[3] ^= 1
+            expect.append((cf.CIO_CORRUPTED, cf.CIO_ERR_BAD_CHECKSUM))
+        elif kind == 3:                       # bytes 6..9 must be zero (8-byte compare)
+            raw[7] = 1
+            expect.append((cf.CIO_CORRUPTED, cf.CIO_ERR_BAD_CHECKSUM))
+        else:
+            expect.append((cf.CIO_OK, 0))
+        open(p, "wb").write(bytes(raw))
+        paths.append(p)
+    st, er, crc = cf.verify_paths(paths)
+    assert [(int(a), int(b)) for a, b in zip(st, er)] == expect
+    for p, s, r in zip(paths, st, crc):
+        if s == cf.CIO_OK:
+            raw = open(p, "rb").read()
+            clen = struct.unpack(">I", raw[10:14])[0]
+            mlen = struct.unpack(">H", raw[22:24])[0]
+            assert int(r) == po.crc_update(INIT, raw[22:24 + mlen + clen])

@@ -1,0 +1,94 @@
+"""Multi-process sharding (world_size 2, gloo, CPU): chunk i -> rank i mod 2,
+no collective on the data path, results gathered by index.  Each rank CRCs
+its shard with the library's host crc_update (the CPU drop-in), which is all
+a CPU rank can run; the GPU ranks run the same shard logic in bench.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from chunkio_amd import shard
+from chunkio_amd import workloads as wl
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, seed, q):
+    import torch.distributed as dist
+    import chunkio_amd as cio
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lens = (np.arange(n) * 977 % 20000).astype(np.uint64)
+        ids = shard.shard_ids(n, rank, world)
+        local = np.asarray([cio.crc_update(0xFFFFFFFF, wl.gen_chunk(seed, int(i), int(lens[i])))
+                            for i in ids], dtype=np.uint32)
+        full = shard.gather_results(local, n)
+        only0 = shard.gather_results(local, n, dst=0)
+        if rank == 0:
+            q.put((full, only0))
+        else:
+            assert only0 is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_ids_partition():
+    for n in (0, 1, 7, 1024, 8192):
+        for world in (1, 2, 3, 8):
+            ids = np.concatenate([shard.shard_ids(n, r, world) for r in range(world)])
+            assert sorted(ids.tolist()) == list(range(n))
+    with pytest.raises(ValueError):
+        shard.shard_ids(10, 2, 2)
+
+
+def test_assemble_roundtrip():
+    n, world = 37, 3
+    vals = np.arange(n, dtype=np.uint32) * 7
+    parts = [vals[shard.shard_ids(n, r, world)] for r in range(world)]
+    np.testing.assert_array_equal(shard.assemble(n, world, parts), vals)
+
+
+def test_gloo_world2_sharded_crc():
+    from oracle import pyoracle as po
+    n, seed, world = 101, 0xC1000004, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, only0 = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    lens = (np.arange(n) * 977 % 20000).astype(np.uint64)
+    want = np.asarray([po.crc_update(0xFFFFFFFF, wl.gen_chunk(seed, i, int(lens[i]))) for i in range(n)],
+                      dtype=np.uint32)
+    np.testing.assert_array_equal(full, want)
+    np.testing.assert_array_equal(only0, want)
+
+
+def test_bench_geometry_shards_cover_job():
+    import bench
+    for cfg in ("cfg2", "cfg4"):
+        seen = []
+        for r in range(4):
+            lens, ids, seed, desc, scaling = bench.geometry(cfg, r, 4)
+            seen.append(ids)
+            assert len(lens) == len(ids)
+        allids = np.sort(np.concatenate(seen))
+        if cfg == "cfg4":      # strong scaling: the 8192-chunk job split four ways
+            assert allids.tolist() == list(range(wl.CFG4_N))
+        else:                  # weak scaling: 1024 chunks per GPU
+            assert allids.tolist() == list(range(4 * wl.CFG2_N))
