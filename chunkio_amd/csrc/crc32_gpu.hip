@@ -70,7 +70,42 @@ struct ChunkDesc {
 };
 static_assert(sizeof(ChunkDesc) == 48, "desc layout");
 
+// Where each wave's step range begins: its first chunk and that chunk's
+// descriptor, so a wave starts streaming after ONE scalar load.
+struct WaveStart {
+    ChunkDesc d;
+    uint32_t c;
+    uint32_t pad[3];
+};
+static_assert(sizeof(WaveStart) == 64, "wave start layout");
+
 // ---------------------------------------------------------------- device math
+
+// Compile-time GF(2) arithmetic (same math as crc32_host.c) for table constants.
+constexpr uint32_t cx_multmodp(uint32_t a, uint32_t b)
+{
+    uint32_t p = 0;
+    for (int i = 31; i >= 0; --i) {
+        if ((a >> i) & 1u) {
+            p ^= b;
+        }
+        b = (b & 1u) ? (b >> 1) ^ CIOA_POLY : (b >> 1);
+    }
+    return p;
+}
+
+constexpr uint32_t cx_xpow8n(uint64_t n)
+{
+    uint32_t r = 0x80000000u, sq = 0x00800000u;
+    while (n) {
+        if (n & 1u) {
+            r = cx_multmodp(sq, r);
+        }
+        sq = cx_multmodp(sq, sq);
+        n >>= 1;
+    }
+    return r;
+}
 
 // a(x) * b(x) mod P(x), reflected bit order (bit 31 = x^0).
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b)
@@ -152,6 +187,45 @@ __device__ __forceinline__ uint4 ldg16(const uint8_t *p)
 {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// In-kernel table entries (no global memory on the start-up path):
+//   slice table k, entry b = shift(b, k + 1)          (b advanced k+1 zero bytes)
+//   shift table k, entry b = shift(b << 8k, kStep - kGran)
+// Both are GF(2)-linear in the 8 bits of b, so an entry is the XOR of the
+// images of b's set bits: 8 compile-time constants per table (immediates).
+struct Basis8 {
+    uint32_t v[8];
+    constexpr Basis8(uint32_t mul, int byte_pos) : v{}
+    {
+        for (int j = 0; j < 8; ++j) {
+            v[j] = cx_multmodp(mul, (1u << j) << (8 * byte_pos));
+        }
+    }
+};
+
+template <uint32_t MUL, int BYTE>
+__device__ __forceinline__ uint32_t basis_entry(uint32_t b)
+{
+    constexpr Basis8 B(MUL, BYTE);
+    uint32_t p = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        p ^= B.v[j] & (0u - ((b >> j) & 1u));
+    }
+    return p;
+}
+
+constexpr uint32_t kXStepShift = cx_xpow8n(kStep - kGran);
+
+__device__ __forceinline__ void table_entries(uint32_t k, uint32_t b, uint32_t &slice, uint32_t &shift)
+{
+    switch (k) {
+    case 0: slice = basis_entry<cx_xpow8n(1), 0>(b); shift = basis_entry<kXStepShift, 0>(b); break;
+    case 1: slice = basis_entry<cx_xpow8n(2), 0>(b); shift = basis_entry<kXStepShift, 1>(b); break;
+    case 2: slice = basis_entry<cx_xpow8n(3), 0>(b); shift = basis_entry<kXStepShift, 2>(b); break;
+    default: slice = basis_entry<cx_xpow8n(4), 0>(b); shift = basis_entry<kXStepShift, 3>(b); break;
+    }
 }
 
 // One lane's 4 x 16 bytes of a step: sub-chain q holds [1024 q + 16 lane, +16).
@@ -288,10 +362,10 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
     }
 }
 
-template <int D, bool STAMPS = false, int PRIO = 1>
-__global__ void __launch_bounds__(kThreads, 1)
+template <int D, bool STAMPS = false, int PRIO = 1, int NT = kThreads>
+__global__ void __launch_bounds__(NT, 1)
 crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restrict__ desc,
-                    const uint32_t *__restrict__ wave_chunk0, const uint32_t *__restrict__ tiny,
+                    const WaveStart *__restrict__ wstart, const uint32_t *__restrict__ tiny,
                     const uint32_t *__restrict__ seeds, uint32_t *out, const uint32_t *__restrict__ cid,
                     unsigned long long *__restrict__ partials, uint32_t *__restrict__ counters,
                     const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
@@ -306,12 +380,17 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
         t_entry = __builtin_amdgcn_s_memrealtime();
     }
 
-    // Table words first: vmcnt is in order, so loads issued after them (the
-    // ring prologue) do not delay the table build.
-    const uint32_t tab_v = g_slice[tid];
-    const uint32_t tab_sv = g_shift[tid];
+    // Table entries are computed, not loaded: at kernel start every global
+    // load pays cold-cache latency, and the build sits on the critical path.
+    constexpr int kE = 1024 / NT;            // table entries per thread
+    uint32_t tab_v[kE], tab_sv[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t idx = tid + (uint32_t) NT * e;
+        table_entries(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u, tab_v[e], tab_sv[e]);
+    }
 
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (tid >> 6));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (NT / kWave) + (tid >> 6));
     const uint32_t lane = tid & 63u;
     const uint32_t lb_lo = (lane & 31u) << 2;
     const uint32_t lb_hi = lb_lo | 0x10000u;
@@ -327,8 +406,9 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
     ChunkDesc d = {}, ld = {};
     uint64_t j = 0, lj = 0, nload = 0;
     if (active) {
-        c = wave_chunk0[wave];
-        d = desc[c];
+        const WaveStart ws = wstart[wave];
+        c = ws.c;
+        d = ws.d;
         j = g0 - d.g;
         lc = c;
         ld = d;
@@ -372,19 +452,47 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
         issue(ring[k]);
     }
 
-    {   // Tables: thread tid owns entry b of table k (tid = 256 k + b).
-        const uint32_t k = tid >> 8, b = tid & 255u;
-        const uint32_t v = tab_v;
-        const uint4 v4 = make_uint4(v, v, v, v);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds + ((k >> 1) << 16) + (b << 8) + ((k & 1u) << 7));
+    {   // Tables.  Phase 1: thread tid computes entry b = tid & 255 of slice
+        // table k = tid >> 8 and of shift table k into compact 4 KiB arrays
+        // parked in the shift-table region.  Phase 2: every thread gathers the
+        // 10 entries of its granules.  Phase 3: consecutive lanes write
+        // consecutive 16-byte granules of the replicated images (bank-conflict
+        // free: a thread writing 128 contiguous bytes puts a whole wave on 4 banks).
+        uint32_t *cslice = reinterpret_cast<uint32_t *>(lds + kShiftOff);
+        uint32_t *cshift = cslice + 1024;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            dst[q] = v4;
+        for (int e = 0; e < kE; ++e) {
+            cslice[tid + NT * e] = tab_v[e];
+            cshift[tid + NT * e] = tab_sv[e];
         }
-        const uint32_t sv = tab_sv;
-        uint4 *sd = reinterpret_cast<uint4 *>(lds + kShiftOff + k * 8192u + b * 32u);
-        sd[0] = make_uint4(sv, sv, sv, sv);
-        sd[1] = make_uint4(sv, sv, sv, sv);
+        __syncthreads();
+        constexpr int kSG = 8192 / NT, kHG = 2048 / NT;   // granules per thread
+        uint32_t sv[kSG], hv[kHG];
+#pragma unroll
+        for (int i = 0; i < kSG; ++i) {
+            // slice image granule g: byte address 16 g -> table pair g >> 12,
+            // entry b = (g >> 4) & 255, table half (g >> 3) & 1
+            const uint32_t g = tid + (uint32_t) NT * i;
+            const uint32_t k = 2u * (g >> 12) + ((g >> 3) & 1u);
+            sv[i] = cslice[(k << 8) | ((g >> 4) & 255u)];
+        }
+#pragma unroll
+        for (int i = 0; i < kHG; ++i) {
+            // shift image granule g: byte address 16 g = k*8192 + b*32 + replica
+            const uint32_t g = tid + (uint32_t) NT * i;
+            hv[i] = cshift[((g >> 9) << 8) | ((g >> 1) & 255u)];
+        }
+        __syncthreads();
+        uint4 *img = reinterpret_cast<uint4 *>(lds);
+#pragma unroll
+        for (int i = 0; i < kSG; ++i) {
+            img[tid + (uint32_t) NT * i] = make_uint4(sv[i], sv[i], sv[i], sv[i]);
+        }
+        uint4 *simg = reinterpret_cast<uint4 *>(lds + kShiftOff);
+#pragma unroll
+        for (int i = 0; i < kHG; ++i) {
+            simg[tid + (uint32_t) NT * i] = make_uint4(hv[i], hv[i], hv[i], hv[i]);
+        }
     }
     __syncthreads();
     if (STAMPS) {
@@ -474,7 +582,7 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
         if (STAMPS) {
             t_stream = __builtin_amdgcn_s_memrealtime();
         }
-        uint32_t ac = wave_chunk0[wave];
+        uint32_t ac = wstart[wave].c;
         for (;;) {
             const ChunkDesc ad = desc[ac];
             if (ad.nsteps != 0) {
@@ -666,10 +774,11 @@ struct cio_crc32_plan {
     uint32_t ntiny = 0;        // chunks with len < 4 (byte-serial)
     int ring = kRingDefault;   // CIO_GPU_RING=1..4 overrides (tuning)
     int prio = 1;              // CIO_GPU_PRIO=0 disables the priority rotation
+    int threads = kThreads;    // CIO_GPU_THREADS=512 selects 8-wave workgroups
     unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     ChunkDesc *desc = nullptr;
-    uint32_t *wave_chunk0 = nullptr;
+    WaveStart *wstart = nullptr;
     uint32_t *tiny = nullptr;
     unsigned long long *partials = nullptr;
     uint32_t *counters = nullptr;
@@ -701,7 +810,7 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
         return;
     }
     (void) hipFree(p->desc);
-    (void) hipFree(p->wave_chunk0);
+    (void) hipFree(p->wstart);
     (void) hipFree(p->tiny);
     (void) hipFree(p->partials);
     (void) hipFree(p->counters);
@@ -731,12 +840,17 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     }
     if (const char *r = getenv("CIO_GPU_RING")) {
         const int v = atoi(r);
-        if (v >= 1 && v <= 4) {
+        if (v >= 1 && v <= 3) {
             p->ring = v;
         }
     }
     p->grid = (uint32_t) st->cus;
-    p->W = p->grid * kWavesPerWG;
+    if (const char *r = getenv("CIO_GPU_THREADS")) {
+        if (atoi(r) == 512) {
+            p->threads = 512;
+        }
+    }
+    p->W = p->grid * (p->threads / kWave);
     if (const char *r = getenv("CIO_GPU_STAMPS")) {
         if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * 4 * sizeof(unsigned long long)) != hipSuccess) {
             p->stamps = nullptr;
@@ -792,6 +906,14 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
             }
         }
     }
+    std::vector<WaveStart> ws(p->W);
+    for (uint32_t w = 0; w < p->W; w++) {
+        memset(&ws[w], 0, sizeof(WaveStart));
+        ws[w].c = wc[w];
+        if (n) {
+            ws[w].d = desc[wc[w]];
+        }
+    }
     const uint64_t nx4k = max_steps + 2;
     std::vector<uint32_t> x4k(nx4k);
     cioa_gen_xpow8_table(x4k.data(), nx4k, (uint64_t) kStep);
@@ -799,13 +921,13 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     hipError_t e;
     const size_t npart = (size_t) p->W + n + 1;
     if ((e = hipMalloc(&p->desc, desc.size() * sizeof(ChunkDesc))) != hipSuccess ||
-        (e = hipMalloc(&p->wave_chunk0, wc.size() * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(&p->wstart, ws.size() * sizeof(WaveStart))) != hipSuccess ||
         (e = hipMalloc(&p->tiny, std::max<size_t>(1, tiny.size()) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&p->partials, npart * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&p->counters, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&p->x4k, nx4k * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemcpy(p->desc, desc.data(), desc.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(p->wave_chunk0, wc.data(), wc.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(p->wstart, ws.data(), ws.size() * sizeof(WaveStart), hipMemcpyHostToDevice)) != hipSuccess ||
         (tiny.size() && (e = hipMemcpy(p->tiny, tiny.data(), tiny.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) ||
         (e = hipMemset(p->partials, 0, npart * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMemset(p->counters, 0, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
@@ -859,6 +981,29 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 }  // extern "C"
 
+using StreamKernel = decltype(&crc32_stream_kernel<1, false, 1, 1024>);
+
+template <int NT>
+static StreamKernel select_ring(int ring, int prio, bool stamps)
+{
+    if (stamps) {
+        return prio ? crc32_stream_kernel<1, true, 1, NT> : crc32_stream_kernel<1, true, 0, NT>;
+    }
+    switch (ring * 2 + (prio ? 1 : 0)) {
+    case 2: return crc32_stream_kernel<1, false, 0, NT>;
+    case 4: return crc32_stream_kernel<2, false, 0, NT>;
+    case 5: return crc32_stream_kernel<2, false, 1, NT>;
+    case 6: return crc32_stream_kernel<3, false, 0, NT>;
+    case 7: return crc32_stream_kernel<3, false, 1, NT>;
+    default: return crc32_stream_kernel<1, false, 1, NT>;
+    }
+}
+
+static StreamKernel select_kernel(int ring, int prio, int threads, bool stamps)
+{
+    return threads == 512 ? select_ring<512>(ring, prio, stamps) : select_ring<1024>(ring, prio, stamps);
+}
+
 // One launch: stream kernel (CRC of every step, per-chunk fold by the last
 // arriver, tiny chunks).  The per-chunk counters are self-resetting, so no
 // memset node precedes it and the launch can be captured in a HIP graph.
@@ -879,27 +1024,9 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
-    auto kern = crc32_stream_kernel<kRingDefault, false, 1>;
-    if (p->prio) {
-        switch (p->ring) {
-        case 1: kern = crc32_stream_kernel<1, false, 1>; break;
-        case 2: kern = crc32_stream_kernel<2, false, 1>; break;
-        case 4: kern = crc32_stream_kernel<4, false, 1>; break;
-        default: break;
-        }
-    } else {
-        switch (p->ring) {
-        case 1: kern = crc32_stream_kernel<1, false, 0>; break;
-        case 2: kern = crc32_stream_kernel<2, false, 0>; break;
-        case 4: kern = crc32_stream_kernel<4, false, 0>; break;
-        default: kern = crc32_stream_kernel<kRingDefault, false, 0>; break;
-        }
-    }
-    if (p->stamps) {
-        kern = p->prio ? crc32_stream_kernel<kRingDefault, true, 1> : crc32_stream_kernel<kRingDefault, true, 0>;
-    }
-    hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
-                       reinterpret_cast<const uint8_t *>(dev_base), p->desc, p->wave_chunk0, p->tiny,
+    auto kern = select_kernel(p->ring, p->prio, p->threads, p->stamps != nullptr);
+    hipLaunchKernelGGL(kern, dim3(p->grid), dim3(p->threads), 0, s,
+                       reinterpret_cast<const uint8_t *>(dev_base), p->desc, p->wstart, p->tiny,
                        dev_seeds, dev_out, cid, p->partials, p->counters, st->slice, st->shift,
                        st->x8, p->x4k, p->S, p->W, p->n, p->ntiny, p->stamps);
     HIP_TRY(hipGetLastError(), "crc32_stream_kernel launch");

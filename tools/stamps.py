@@ -42,6 +42,11 @@ def main():
         print("   exit       ", q(us[:, 3]))
         print("   stream dur ", q(us[:, 2] - us[:, 1]))
         print("   tail dur   ", q(us[:, 3] - us[:, 2]))
+        ent = us[:, 0].reshape(-1, 16)
+        tab = us[:, 1].reshape(-1, 16)
+        print("   WG entry spread (last-first wave)", q(ent.max(1) - ent.min(1)))
+        print("   WG first entry                   ", q(ent.min(1)))
+        print("   WG tables - last entry           ", q(tab.max(1) - ent.max(1)))
         wg = us[:, 2].reshape(-1, 16)
         print("   WG max done", q(wg.max(1)))
         print("   WG min done", q(wg.min(1)))

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """A/B sweep of kernel variants, interleaved in one process (guide rule 24).
 
-    python tools/sweep.py [--iters 20] [--rounds 3] [--var CIO_GPU_RING=1,2,3,4] [--cfg cfg2,big]
+    python tools/sweep.py [--iters 20] [--rounds 3] [--var CIO_GPU_RING=1,2,3] [--cfg cfg2,big]
+    python tools/sweep.py --variants "CIO_GPU_THREADS=1024|CIO_GPU_THREADS=512,CIO_GPU_RING=2"
 
-Each variant is a plan created with the given environment variable set (the
+Each variant is a plan created with the given environment variables set (the
 library reads tuning knobs at plan creation).  Every variant's output is
 checked equal to the first variant's; per round and variant the mean kernel
 time over `iters` launches (HIP events around the kernel) is printed, then the
@@ -25,14 +26,29 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--var", default="CIO_GPU_RING=1,2,3,4")
+    ap.add_argument("--variants", default=None,
+                    help="'|'-separated variants, each a comma-separated list of VAR=value")
     ap.add_argument("--cfg", default="cfg2,big")
     args = ap.parse_args()
     import torch
     import chunkio_amd as cio
     from chunkio_amd import workloads as wl
 
-    name, vals = args.var.split("=")
-    vals = vals.split(",")
+    if args.variants:
+        vals = args.variants.split("|")
+        name = "variant"
+    else:
+        name, v = args.var.split("=")
+        vals = [f"{name}={x}" for x in v.split(",")]
+
+    def apply(v):
+        for kv in v.split(","):
+            k, x = kv.split("=")
+            os.environ[k] = x
+
+    def clear(v):
+        for kv in v.split(","):
+            os.environ.pop(kv.split("=")[0], None)
     dev = torch.device("cuda:0")
     lib = cio.lib()
     results = {}
@@ -58,9 +74,9 @@ def main():
         out = torch.empty(len(lens), dtype=torch.int32, device=dev)
         plans = {}
         for v in vals:
-            os.environ[name] = v
+            apply(v)
             plans[v] = cio.Crc32Plan(offs, lens)
-        os.environ.pop(name, None)
+            clear(v)
         ref = None
         for v in vals:
             plans[v].exec(bufs[0], out)
@@ -80,11 +96,11 @@ def main():
                 torch.cuda.synchronize()
                 ms = float(np.mean([lib.cio_gpu_event_elapsed_ms(a, b) for a, b in evs]))
                 times[v].append(ms * 1e3)
-                print(f"{cfg} round {r} {name}={v}: {ms * 1e3:8.2f} us  {total / ms / 1e6:8.1f} GB/s",
+                print(f"{cfg} round {r} {v}: {ms * 1e3:8.2f} us  {total / ms / 1e6:8.1f} GB/s",
                       flush=True)
         for v in vals:
             med = float(np.median(times[v]))
-            results[f"{cfg}/{name}={v}"] = {"us": round(med, 2), "GBps": round(total / med / 1e3, 1)}
+            results[f"{cfg}/{v}"] = {"us": round(med, 2), "GBps": round(total / med / 1e3, 1)}
         for p in plans.values():
             p.close()
         del bufs
