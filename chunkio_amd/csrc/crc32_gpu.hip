@@ -52,7 +52,6 @@ constexpr int kSub = 4;                     // sub-chains per lane
 constexpr int kRow = kWave * kGran;         // 1024: one coalesced wave-instruction
 constexpr int kStep = kSub * kRow;          // 4096 bytes per wave-step
 constexpr int kThreads = 1024;              // one workgroup per CU
-constexpr int kWavesPerWG = kThreads / kWave;
 constexpr int kX8Count = 2 * kStep;         // x^(8m), m in [0, 8192)
 constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
@@ -296,13 +295,6 @@ __device__ __forceinline__ void slow_compute(const char *lds, uint32_t lb_lo, ui
     }
 }
 
-__device__ __forceinline__ uint32_t xpow8_bytes(uint64_t bytes, const uint32_t *x8, const uint32_t *x4k)
-{
-    const uint64_t m = bytes / kStep;
-    const uint32_t r = (uint32_t) (bytes % kStep);
-    return m == 0 ? x8[r] : multmodp(x4k[m], x8[r]);
-}
-
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
 #pragma unroll
@@ -314,24 +306,22 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 
 // All pieces of chunk c folded into one raw CRC by the last wave to publish
 // one: XOR over pieces of shift(piece, bytes after it), lanes in parallel.
-__device__ __forceinline__ void fold_chunk(const ChunkDesc &d, uint32_t c, uint32_t oc, uint32_t lane,
-                                           const unsigned long long *partials, uint32_t *out,
-                                           uint32_t *counters, const uint32_t *g_x8,
-                                           const uint32_t *g_x4k, uint64_t S, uint32_t W)
+// The shift factors x^(8 * bytes after the piece) are per piece slot and
+// precomputed by the plan, so a fold is one round of independent loads.
+__device__ __forceinline__ void fold_chunk(uint64_t g, uint32_t nsteps, uint32_t c, uint32_t oc,
+                                           uint32_t lane, const unsigned long long *partials,
+                                           const uint32_t *pfac, uint32_t *out, uint32_t *counters,
+                                           uint64_t S, uint32_t W)
 {
-    const uint64_t w0 = wave_of_step(d.g, S, W);
-    const uint64_t w1 = wave_of_step(d.g + d.nsteps - 1, S, W);
+    const uint64_t w0 = wave_of_step(g, S, W);
+    const uint64_t w1 = wave_of_step(g + nsteps - 1, S, W);
     uint32_t acc = 0;
     for (uint64_t wb = w0; wb <= w1; wb += kWave) {
         const uint64_t wv = wb + lane;
-        if (wv <= w1) {
-            const uint64_t st = wave_start(wv, S, W), en = wave_start(wv + 1, S, W);
-            if (st < en) {
-                const uint32_t p = (uint32_t) __hip_atomic_load(&partials[wv + c], __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t pend = min(min(en - d.g, (uint64_t) d.nsteps) * kStep, d.vlen);
-                acc ^= p ? multmodp(xpow8_bytes(d.vlen - pend, g_x8, g_x4k), p) : 0u;
-            }
+        if (wv <= w1 && wave_start(wv, S, W) < wave_start(wv + 1, S, W)) {
+            const uint32_t p = (uint32_t) __hip_atomic_load(&partials[wv + c], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+            acc ^= multmodp(pfac[wv + c], p);
         }
     }
     acc = wave_xor(acc);
@@ -364,12 +354,12 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 
 template <int D, bool STAMPS = false, int PRIO = 1, int NT = kThreads>
 __global__ void __launch_bounds__(NT, 1)
-crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restrict__ desc,
+crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
                     const WaveStart *__restrict__ wstart, const uint32_t *__restrict__ tiny,
                     const uint32_t *__restrict__ seeds, uint32_t *out, const uint32_t *__restrict__ cid,
                     unsigned long long *__restrict__ partials, uint32_t *__restrict__ counters,
                     const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
-                    const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_x4k,
+                    const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ pfac,
                     uint64_t S, uint32_t W, uint32_t n, uint32_t ntiny,
                     unsigned long long *stamps = nullptr)
 {
@@ -402,12 +392,13 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
 
     // Compute cursor (c, d, j) and load cursor (lc, ld, lj) walk the same
     // step sequence; the load cursor runs D steps ahead.
-    uint32_t c = 0, lc = 0;
+    uint32_t c = 0, lc = 0, c0 = 0;
     ChunkDesc d = {}, ld = {};
     uint64_t j = 0, lj = 0, nload = 0;
     if (active) {
         const WaveStart ws = wstart[wave];
         c = ws.c;
+        c0 = c;
         d = ws.d;
         j = g0 - d.g;
         lc = c;
@@ -451,6 +442,19 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
     for (int k = 0; k < D; ++k) {
         issue(ring[k]);
     }
+    // Descriptors of the first 64 chunks from c0 (one per lane) for the
+    // arrival step at the end; fetched now so that they cost nothing there.
+    // Clamped, not predicated: a branch would break the ring's vmcnt tracking.
+    uint64_t ar_g;
+    uint32_t ar_ns, ar_np;
+    {
+        const ChunkDesc &ad = desc[min(c0 + lane, n - 1)];
+        ar_g = ad.g;
+        ar_ns = ad.nsteps;
+        ar_np = ad.npieces;
+    }
+    // Keep the scheduler from sinking these loads below the table build.
+    __builtin_amdgcn_sched_barrier(0);
 
     {   // Tables.  Phase 1: thread tid computes entry b = tid & 255 of slice
         // table k = tid >> 8 and of shift table k into compact 4 KiB arrays
@@ -582,27 +586,34 @@ crc32_stream_kernel(const uint8_t *__restrict__ base, const ChunkDesc *__restric
         if (STAMPS) {
             t_stream = __builtin_amdgcn_s_memrealtime();
         }
-        uint32_t ac = wstart[wave].c;
-        for (;;) {
-            const ChunkDesc ad = desc[ac];
-            if (ad.nsteps != 0) {
-                if (ad.g >= gend) {
-                    break;
-                }
-                uint32_t old = 0;
-                if (lane == 0) {
-                    old = __hip_atomic_fetch_add(&counters[ac], 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-                }
-                old = __shfl(old, 0);
-                if (old + 1 == ad.npieces) {
-                    fold_chunk(ad, ac, cid ? cid[ac] : ac, lane, partials, out, counters, g_x8, g_x4k,
-                               S, W);
-                }
+        // Lane-parallel: lane i arrives on chunk ac + i when the range holds
+        // a piece of it; the batch of 64 ends the scan if it reaches a
+        // non-empty chunk that starts past the range (or the end of the batch).
+        for (uint32_t ac = c0;;) {
+            const uint32_t idx = ac + lane;
+            const bool inb = idx < n;
+            const bool member = inb && ar_ns != 0 && ar_g < gend;
+            const bool stop = !inb || (ar_ns != 0 && ar_g >= gend);
+            uint32_t old = 0;
+            if (member) {
+                old = __hip_atomic_fetch_add(&counters[idx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (++ac >= n) {
+            for (uint64_t fin = __ballot(member && old + 1 == ar_np); fin; fin &= fin - 1) {
+                const uint32_t b = (uint32_t) __builtin_ctzll(fin);
+                const uint32_t fc = ac + b;
+                const uint64_t fg = ((uint64_t) __builtin_amdgcn_readlane((uint32_t) (ar_g >> 32), b) << 32) |
+                                    __builtin_amdgcn_readlane((uint32_t) ar_g, b);
+                fold_chunk(fg, __builtin_amdgcn_readlane(ar_ns, b), fc, cid ? cid[fc] : fc, lane,
+                           partials, pfac, out, counters, S, W);
+            }
+            if (__ballot(stop)) {
                 break;
             }
+            ac += kWave;
+            const ChunkDesc &ad = desc[min(ac + lane, n - 1)];
+            ar_g = ad.g;
+            ar_ns = ad.nsteps;
+            ar_np = ad.npieces;
         }
     }
 
@@ -782,7 +793,7 @@ struct cio_crc32_plan {
     uint32_t *tiny = nullptr;
     unsigned long long *partials = nullptr;
     uint32_t *counters = nullptr;
-    uint32_t *x4k = nullptr;
+    uint32_t *pfac = nullptr;   // per piece slot: x^(8 * chunk bytes after the piece)
     DeviceState *st = nullptr;
 };
 
@@ -814,7 +825,7 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
     (void) hipFree(p->tiny);
     (void) hipFree(p->partials);
     (void) hipFree(p->counters);
-    (void) hipFree(p->x4k);
+    (void) hipFree(p->pfac);
     (void) hipFree(p->stamps);
     delete p;
 }
@@ -859,7 +870,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
 
     std::vector<ChunkDesc> desc(n ? n : 1);
     std::vector<uint32_t> tiny;
-    uint64_t S = 0, bytes = 0, max_steps = 0;
+    uint64_t S = 0, bytes = 0;
     for (size_t i = 0; i < n; i++) {
         ChunkDesc &d = desc[i];
         memset(&d, 0, sizeof(d));
@@ -878,7 +889,6 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         }
         S += ns;
         bytes += lens[i];
-        max_steps = std::max(max_steps, ns);
     }
     p->S = S;
     p->bytes = bytes;
@@ -887,6 +897,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // First non-empty chunk of every wave's step range, and per chunk the
     // number of (non-empty) waves that hold a piece of it.
     std::vector<uint32_t> wc(p->W, 0);
+    std::vector<uint32_t> pfac((size_t) p->W + n + 1, 0);
     if (S > 0) {
         size_t c = 0;
         for (uint32_t w = 0; w < p->W; w++) {
@@ -902,6 +913,9 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
             for (size_t k = c; k < n && desc[k].g < g1; k++) {
                 if (desc[k].nsteps) {
                     desc[k].npieces++;
+                    const uint64_t pend = std::min(std::min(g1 - desc[k].g, (uint64_t) desc[k].nsteps) *
+                                                   (uint64_t) kStep, desc[k].vlen);
+                    pfac[w + k] = cioa_xpow8n(desc[k].vlen - pend);
                 }
             }
         }
@@ -914,10 +928,6 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
             ws[w].d = desc[wc[w]];
         }
     }
-    const uint64_t nx4k = max_steps + 2;
-    std::vector<uint32_t> x4k(nx4k);
-    cioa_gen_xpow8_table(x4k.data(), nx4k, (uint64_t) kStep);
-
     hipError_t e;
     const size_t npart = (size_t) p->W + n + 1;
     if ((e = hipMalloc(&p->desc, desc.size() * sizeof(ChunkDesc))) != hipSuccess ||
@@ -925,13 +935,13 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         (e = hipMalloc(&p->tiny, std::max<size_t>(1, tiny.size()) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&p->partials, npart * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&p->counters, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMalloc(&p->x4k, nx4k * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(&p->pfac, pfac.size() * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemcpy(p->desc, desc.data(), desc.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->wstart, ws.data(), ws.size() * sizeof(WaveStart), hipMemcpyHostToDevice)) != hipSuccess ||
         (tiny.size() && (e = hipMemcpy(p->tiny, tiny.data(), tiny.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) ||
         (e = hipMemset(p->partials, 0, npart * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMemset(p->counters, 0, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMemcpy(p->x4k, x4k.data(), nx4k * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) {
+        (e = hipMemcpy(p->pfac, pfac.data(), pfac.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) {
         cio_crc32_plan_destroy(p);
         return fail("cio_crc32_plan_create: device allocation/upload", e);
     }
@@ -1028,7 +1038,7 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(p->threads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->desc, p->wstart, p->tiny,
                        dev_seeds, dev_out, cid, p->partials, p->counters, st->slice, st->shift,
-                       st->x8, p->x4k, p->S, p->W, p->n, p->ntiny, p->stamps);
+                       st->x8, p->pfac, p->S, p->W, p->n, p->ntiny, p->stamps);
     HIP_TRY(hipGetLastError(), "crc32_stream_kernel launch");
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");
