@@ -19,7 +19,7 @@ EXPORTS = (
     "cio_crc32_shift", "cio_crc32_combine",
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_batch_dev", "cio_crc32_batch_host",
-    "cio_gpu_fill_synthetic", "cio_sha1_batch_dev",
+    "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_gpu_read_stream",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
     # include/chunkio_amd/cio_verify.h
@@ -52,6 +52,7 @@ def _bind(lib):
         "cio_gpu_fill_synthetic": (ctypes.c_int, [V, c_u64_p, c_u64_p, c_u64_p, ctypes.c_size_t,
                                                   ctypes.c_uint64, V]),
         "cio_sha1_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, ctypes.c_size_t, V]),
+        "cio_gpu_read_stream": (ctypes.c_int, [V, ctypes.c_uint64, V]),
         "cio_gpu_event_create": (V, []),
         "cio_gpu_event_destroy": (None, [V]),
         "cio_gpu_event_record": (ctypes.c_int, [V, V]),

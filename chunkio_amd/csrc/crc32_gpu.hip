@@ -639,6 +639,33 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
     }
 }
 
+// ---------------------------------------------------------------- read-only stream
+
+// Practical HBM-read ceiling for the CRC kernel's access pattern: the same
+// persistent grid (one 1024-thread workgroup per CU), the same even split of
+// 4 KiB wave-steps and the same coalesced non-temporal 16-byte loads, with the
+// CRC replaced by an XOR.  One 4-byte store per wave keeps the loads live.
+__global__ void __launch_bounds__(kThreads, 1)
+read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__restrict__ sink)
+{
+    const uint32_t W = gridDim.x * (kThreads / kWave);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    for (uint64_t g = g0; g < g1; ++g) {
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * kGran);
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+            acc ^= __builtin_nontemporal_load(p + q * kWave);
+        }
+    }
+    const uint32_t x = wave_xor(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]);
+    if (lane == 0) {
+        sink[wave] = x;
+    }
+}
+
 // ---------------------------------------------------------------- synthetic fill
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
@@ -1097,6 +1124,27 @@ int cio_gpu_fill_synthetic(void *dev_base, const uint64_t *offs, const uint64_t 
     if (e != hipSuccess) {
         return fail("fill_kernel", e);
     }
+    return CIO_OK;
+}
+
+int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
+{
+    DeviceState *st;
+    if (device_state(&st) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    static thread_local uint32_t *sink = nullptr;
+    if (!sink) {
+        HIP_TRY(hipMalloc(&sink, 65536 * sizeof(uint32_t)), "read_stream: hipMalloc");
+    }
+    const uint64_t S = bytes / kStep;
+    if (S == 0 || dev_base == nullptr) {
+        return CIO_OK;
+    }
+    hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const uint8_t *>(dev_base), S, sink);
+    HIP_TRY(hipGetLastError(), "read_stream_kernel launch");
     return CIO_OK;
 }
 

@@ -135,6 +135,13 @@ int  cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs,
                         const uint64_t *lens, uint8_t *dev_digests, size_t n,
                         void *stream);
 
+/* ---- diagnostics -------------------------------------------------------- */
+
+/* Read-only stream over floor(bytes / 4096) * 4096 bytes of dev_base with the
+ * CRC kernel's grid and load pattern (no CRC): the practical HBM-read ceiling
+ * the CRC kernel is measured against.  Asynchronous on `stream`. */
+int  cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream);
+
 /* ---- timing helpers (HIP events on a given stream) --------------------- */
 
 void  *cio_gpu_event_create(void);
