@@ -857,20 +857,13 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
     delete p;
 }
 
-int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint64_t *lens, size_t n)
+}  // extern "C"
+
+namespace {
+
+// Tuning knobs (environment, read at plan creation) and grid geometry.
+void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
 {
-    if (!out || (n && (!offs || !lens))) {
-        return fail("cio_crc32_plan_create: null argument");
-    }
-    if (n >= 0xffffffffull) {
-        return fail("cio_crc32_plan_create: too many chunks");
-    }
-    *out = nullptr;
-    DeviceState *st;
-    if (device_state(&st) != CIO_OK) {
-        return CIO_ERROR;
-    }
-    cio_crc32_plan *p = new cio_crc32_plan();
     p->st = st;
     p->n = (uint32_t) n;
     if (const char *r = getenv("CIO_GPU_PRIO")) {
@@ -889,86 +882,151 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         }
     }
     p->W = p->grid * (p->threads / kWave);
-    if (const char *r = getenv("CIO_GPU_STAMPS")) {
-        if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * 4 * sizeof(unsigned long long)) != hipSuccess) {
-            p->stamps = nullptr;
-        }
-    }
+}
 
-    std::vector<ChunkDesc> desc(n ? n : 1);
+// Host image of everything a launch reads besides the data.
+struct PlanHost {
+    std::vector<ChunkDesc> desc;
+    std::vector<WaveStart> ws;
     std::vector<uint32_t> tiny;
+    std::vector<uint32_t> pfac;   // per piece slot (wave + chunk)
+    uint64_t S = 0, bytes = 0;
+};
+
+// Virtual aligned chunks, wave-step numbering, the even split of the S steps
+// over W waves, each wave's first chunk, per-chunk piece counts and per-slot
+// fold factors.  Host only; returns an error message or nullptr.
+const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens, size_t n, uint32_t W)
+{
+    ph.desc.assign(n ? n : 1, ChunkDesc{});
+    ph.tiny.clear();
     uint64_t S = 0, bytes = 0;
     for (size_t i = 0; i < n; i++) {
-        ChunkDesc &d = desc[i];
-        memset(&d, 0, sizeof(d));
+        ChunkDesc &d = ph.desc[i];
         d.a = offs[i] & ~15ull;
         d.h = (uint32_t) (offs[i] & 15u);
         d.vlen = d.h + lens[i];
         d.g = S;
         const uint64_t ns = lens[i] >= 4 ? (d.vlen + kStep - 1) / kStep : 0;
         if (ns > 0xffffffffull) {
-            delete p;
-            return fail("cio_crc32_plan_create: chunk too large");
+            return "cio_crc32_plan_create: chunk too large";
         }
         d.nsteps = (uint32_t) ns;
         if (ns == 0) {
-            tiny.push_back((uint32_t) i);
+            ph.tiny.push_back((uint32_t) i);
         }
         S += ns;
         bytes += lens[i];
     }
-    p->S = S;
-    p->bytes = bytes;
-    p->ntiny = (uint32_t) tiny.size();
+    ph.S = S;
+    ph.bytes = bytes;
 
-    // First non-empty chunk of every wave's step range, and per chunk the
-    // number of (non-empty) waves that hold a piece of it.
-    std::vector<uint32_t> wc(p->W, 0);
-    std::vector<uint32_t> pfac((size_t) p->W + n + 1, 0);
+    // Fold factors x^(8 d) for d = bytes after a piece = 4096 m + r: one
+    // multiply of two table entries (x8 static, x4k per plan up to the
+    // longest chunk) instead of a square-and-multiply per piece.
+    static const std::vector<uint32_t> x8 = [] {
+        std::vector<uint32_t> t(kStep);
+        cioa_gen_xpow8_table(t.data(), kStep, 1);
+        return t;
+    }();
+    uint64_t max_steps = 0;
+    for (size_t i = 0; i < n; i++) {
+        max_steps = std::max<uint64_t>(max_steps, ph.desc[i].nsteps);
+    }
+    std::vector<uint32_t> x4k;
+    if (max_steps <= (1u << 20)) {
+        x4k.resize(max_steps + 1);
+        cioa_gen_xpow8_table(x4k.data(), x4k.size(), (uint64_t) kStep);
+    }
+    auto factor = [&](uint64_t d) {
+        const uint64_t m = d / kStep, r = d % kStep;
+        if (m == 0) {
+            return x8[r];
+        }
+        return m < x4k.size() ? cioa_multmodp(x4k[m], x8[r]) : cioa_xpow8n(d);
+    };
+
+    std::vector<uint32_t> wc(W, 0);
+    ph.pfac.assign((size_t) W + n + 1, 0u);
     if (S > 0) {
         size_t c = 0;
-        for (uint32_t w = 0; w < p->W; w++) {
-            const uint64_t g0 = ((uint64_t) w * S) / p->W;
-            const uint64_t g1 = ((uint64_t) (w + 1) * S) / p->W;
-            while (c < n && (desc[c].nsteps == 0 || desc[c].g + desc[c].nsteps <= g0)) {
+        for (uint32_t w = 0; w < W; w++) {
+            const uint64_t g0 = ((uint64_t) w * S) / W;
+            const uint64_t g1 = ((uint64_t) (w + 1) * S) / W;
+            while (c < n && (ph.desc[c].nsteps == 0 || ph.desc[c].g + ph.desc[c].nsteps <= g0)) {
                 c++;
             }
             wc[w] = (uint32_t) std::min(c, n - 1);
             if (g0 == g1) {
                 continue;
             }
-            for (size_t k = c; k < n && desc[k].g < g1; k++) {
-                if (desc[k].nsteps) {
-                    desc[k].npieces++;
-                    const uint64_t pend = std::min(std::min(g1 - desc[k].g, (uint64_t) desc[k].nsteps) *
-                                                   (uint64_t) kStep, desc[k].vlen);
-                    pfac[w + k] = cioa_xpow8n(desc[k].vlen - pend);
+            for (size_t k = c; k < n && ph.desc[k].g < g1; k++) {
+                ChunkDesc &d = ph.desc[k];
+                if (d.nsteps) {
+                    d.npieces++;
+                    const uint64_t pend = std::min(std::min(g1 - d.g, (uint64_t) d.nsteps) * (uint64_t) kStep,
+                                                   d.vlen);
+                    ph.pfac[w + k] = factor(d.vlen - pend);
                 }
             }
         }
     }
-    std::vector<WaveStart> ws(p->W);
-    for (uint32_t w = 0; w < p->W; w++) {
-        memset(&ws[w], 0, sizeof(WaveStart));
-        ws[w].c = wc[w];
+    ph.ws.assign(W, WaveStart{});
+    for (uint32_t w = 0; w < W; w++) {
+        ph.ws[w].c = wc[w];
         if (n) {
-            ws[w].d = desc[wc[w]];
+            ph.ws[w].d = ph.desc[wc[w]];
+        }
+    }
+    return nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint64_t *lens, size_t n)
+{
+    if (!out || (n && (!offs || !lens))) {
+        return fail("cio_crc32_plan_create: null argument");
+    }
+    if (n >= 0xffffffffull) {
+        return fail("cio_crc32_plan_create: too many chunks");
+    }
+    *out = nullptr;
+    DeviceState *st;
+    if (device_state(&st) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    cio_crc32_plan *p = new cio_crc32_plan();
+    plan_init(p, st, n);
+    PlanHost ph;
+    if (const char *err = plan_build(ph, offs, lens, n, p->W)) {
+        delete p;
+        return fail(err);
+    }
+    p->S = ph.S;
+    p->bytes = ph.bytes;
+    p->ntiny = (uint32_t) ph.tiny.size();
+    if (const char *r = getenv("CIO_GPU_STAMPS")) {
+        if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * 4 * sizeof(unsigned long long)) != hipSuccess) {
+            p->stamps = nullptr;
         }
     }
     hipError_t e;
-    const size_t npart = (size_t) p->W + n + 1;
-    if ((e = hipMalloc(&p->desc, desc.size() * sizeof(ChunkDesc))) != hipSuccess ||
-        (e = hipMalloc(&p->wstart, ws.size() * sizeof(WaveStart))) != hipSuccess ||
-        (e = hipMalloc(&p->tiny, std::max<size_t>(1, tiny.size()) * sizeof(uint32_t))) != hipSuccess ||
+    const size_t npart = ph.pfac.size();
+    if ((e = hipMalloc(&p->desc, ph.desc.size() * sizeof(ChunkDesc))) != hipSuccess ||
+        (e = hipMalloc(&p->wstart, ph.ws.size() * sizeof(WaveStart))) != hipSuccess ||
+        (e = hipMalloc(&p->tiny, std::max<size_t>(1, ph.tiny.size()) * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&p->partials, npart * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&p->counters, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMalloc(&p->pfac, pfac.size() * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMemcpy(p->desc, desc.data(), desc.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(p->wstart, ws.data(), ws.size() * sizeof(WaveStart), hipMemcpyHostToDevice)) != hipSuccess ||
-        (tiny.size() && (e = hipMemcpy(p->tiny, tiny.data(), tiny.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) ||
+        (e = hipMalloc(&p->pfac, npart * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMemcpy(p->desc, ph.desc.data(), ph.desc.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(p->wstart, ph.ws.data(), ph.ws.size() * sizeof(WaveStart), hipMemcpyHostToDevice)) != hipSuccess ||
+        (ph.tiny.size() && (e = hipMemcpy(p->tiny, ph.tiny.data(), ph.tiny.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) ||
         (e = hipMemset(p->partials, 0, npart * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMemset(p->counters, 0, std::max<size_t>(1, n) * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMemcpy(p->pfac, pfac.data(), pfac.size() * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) {
+        (e = hipMemcpy(p->pfac, ph.pfac.data(), npart * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess) {
         cio_crc32_plan_destroy(p);
         return fail("cio_crc32_plan_create: device allocation/upload", e);
     }
@@ -1195,56 +1253,275 @@ int cio_gpu_stream_sync(void *stream)
 // ---------------------------------------------------------------- host-memory batch
 //
 // End-to-end path for chunks that live in host memory (mmap'd chunk files,
-// src/cio_file_unix.c:100): the batch is cut into segments of at most
-// kStage bytes, packed into groups; each group is copied by host threads into
-// one of two pinned staging buffers, sent with hipMemcpyAsync to one of two
-// device buffers, and CRC'd by a plan whose seeds/outputs go through a
-// chunk-id map into one running-state array on the device, so a chunk split
-// over several groups chains its state on the GPU with no host round trip.
-// Copies of group g+1 overlap the kernels of group g.
+// src/cio_file_unix.c:100).  The batch is cut into segments of at most kStage
+// bytes packed into groups.  A persistent per-device pipeline of kSlots slots
+// (pinned staging buffer, pinned plan image, device buffer, device plan
+// arena, stream) carries the groups: host threads copy group g into a free
+// slot while the DMA engine moves group g-1 and the GPU CRCs group g-2.  Each
+// group's plan is built on the host straight into the slot's pinned image and
+// uploaded with the data, so steady-state calls allocate nothing.  Seeds and
+// outputs go through a chunk-id map into one running-state array on the
+// device, so a chunk split over several groups chains its state on the GPU.
 
 #include <thread>
+#include <condition_variable>
 
 namespace {
 
 constexpr size_t kStage = 64ull << 20;
+constexpr int kSlots = 3;
 
 struct HostGroup {
     std::vector<const uint8_t *> src;
     std::vector<uint64_t> offs, lens;
     std::vector<uint32_t> cid;
     uint64_t bytes = 0;
-    cio_crc32_plan *plan = nullptr;
-    uint32_t *d_cid = nullptr;
 };
 
-void parallel_copy(uint8_t *dst, const HostGroup &g)
-{
-    const size_t nthreads = std::min<size_t>(8, std::max<size_t>(1, g.bytes >> 22));
-    if (nthreads <= 1) {
-        for (size_t k = 0; k < g.src.size(); k++) {
-            memcpy(dst + g.offs[k], g.src[k], g.lens[k]);
+// Persistent host copy workers (the box's CPU share per GPU is 16 threads).
+// copy() splits a group's byte range evenly over the workers and the caller,
+// and returns when every slice is in the pinned buffer.
+class CopyPool {
+public:
+    CopyPool()
+    {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned nw = std::min(15u, hw > 1 ? hw - 1 : 0u);
+        for (unsigned t = 0; t < nw; t++) {
+            workers_.emplace_back([this, t]() { run(t + 1); });
         }
-        return;
     }
-    // Split the group's byte range evenly; each thread copies its slice.
-    std::vector<std::thread> th;
-    const uint64_t per = (g.bytes + nthreads - 1) / nthreads;
-    for (size_t t = 0; t < nthreads; t++) {
-        th.emplace_back([&, t]() {
-            const uint64_t lo = t * per, hi = std::min<uint64_t>(g.bytes, lo + per);
-            for (size_t k = 0; k < g.src.size(); k++) {
-                const uint64_t a = g.offs[k], b = a + g.lens[k];
-                const uint64_t x = std::max(a, lo), y = std::min(b, hi);
-                if (x < y) {
-                    memcpy(dst + x, g.src[k] + (x - a), y - x);
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &w : workers_) {
+            w.join();
+        }
+    }
+    void copy(uint8_t *dst, const HostGroup &g)
+    {
+        const size_t parts = std::min<size_t>(workers_.size() + 1, std::max<size_t>(1, g.bytes >> 22));
+        if (parts <= 1) {
+            slice(dst, g, 0, 1);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            dst_ = dst;
+            g_ = &g;
+            parts_ = parts;
+            pending_ = parts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        slice(dst, g, 0, parts);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+private:
+    static void slice(uint8_t *dst, const HostGroup &g, size_t t, size_t parts)
+    {
+        const uint64_t per = (g.bytes + parts - 1) / parts;
+        const uint64_t lo = t * per, hi = std::min<uint64_t>(g.bytes, lo + per);
+        for (size_t k = 0; k < g.src.size(); k++) {
+            const uint64_t a = g.offs[k], b = a + g.lens[k];
+            const uint64_t x = std::max(a, lo), y = std::min(b, hi);
+            if (x < y) {
+                memcpy(dst + x, g.src[k] + (x - a), y - x);
+            }
+        }
+    }
+    void run(size_t id)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            uint8_t *dst;
+            const HostGroup *g;
+            size_t parts;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) {
+                    return;
+                }
+                seen = gen_;
+                dst = dst_;
+                g = g_;
+                parts = parts_;
+            }
+            if (id < parts) {
+                slice(dst, *g, id, parts);
+                std::lock_guard<std::mutex> lk(mu_);
+                if (--pending_ == 0) {
+                    done_cv_.notify_one();
                 }
             }
-        });
+        }
     }
-    for (auto &t : th) {
-        t.join();
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    bool stop_ = false;
+    uint64_t gen_ = 0;
+    uint8_t *dst_ = nullptr;
+    const HostGroup *g_ = nullptr;
+    size_t parts_ = 0, pending_ = 0;
+};
+
+size_t align256(size_t x)
+{
+    return (x + 255) & ~(size_t) 255;
+}
+
+struct PipeSlot {
+    uint8_t *pinned = nullptr;       // kStage data
+    uint8_t *dbuf = nullptr;         // kStage + 64
+    uint8_t *meta_h = nullptr;       // pinned plan image
+    uint8_t *meta_d = nullptr;       // device plan image
+    size_t meta_cap = 0;
+    unsigned long long *partials = nullptr;
+    size_t part_cap = 0;
+    uint32_t *counters = nullptr;    // zero between launches (self-resetting)
+    size_t cnt_cap = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;       // after the slot's kernel
+    bool busy = false;
+};
+
+struct HostPipe {
+    std::mutex mu;
+    bool ready = false;
+    CopyPool *pool = nullptr;
+    PipeSlot slot[kSlots];
+    uint32_t *state = nullptr;       // running raw CRC per chunk of the call
+    size_t state_cap = 0;
+};
+
+std::mutex g_pipe_mu;
+std::vector<HostPipe *> g_pipes;
+
+hipError_t pipe_get(HostPipe **out)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) {
+        return e;
     }
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    if ((int) g_pipes.size() <= dev) {
+        g_pipes.resize(dev + 1, nullptr);
+    }
+    if (!g_pipes[dev]) {
+        g_pipes[dev] = new HostPipe();
+    }
+    *out = g_pipes[dev];
+    return hipSuccess;
+}
+
+hipError_t pipe_init(HostPipe &hp)
+{
+    hipError_t e = hipSuccess;
+    for (int b = 0; b < kSlots && e == hipSuccess; b++) {
+        PipeSlot &s = hp.slot[b];
+        if ((e = hipHostMalloc(&s.pinned, kStage, hipHostMallocDefault)) != hipSuccess) break;
+        if ((e = hipMalloc(&s.dbuf, kStage + 64)) != hipSuccess) break;
+        if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess) break;
+        e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    }
+    if (e == hipSuccess) {
+        hp.pool = new CopyPool();
+    }
+    hp.ready = e == hipSuccess;
+    return e;
+}
+
+template <typename T>
+hipError_t grow_dev(T **p, size_t *cap, size_t need, bool zero, hipStream_t s)
+{
+    if (need <= *cap) {
+        return hipSuccess;
+    }
+    need = std::max(need, *cap * 2);
+    (void) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, need * sizeof(T));
+    if (e == hipSuccess && zero) {
+        e = hipMemsetAsync(*p, 0, need * sizeof(T), s);
+    }
+    if (e == hipSuccess) {
+        *cap = need;
+    }
+    return e;
+}
+
+hipError_t grow_meta(PipeSlot &s, size_t need)
+{
+    if (need <= s.meta_cap) {
+        return hipSuccess;
+    }
+    need = std::max(need, s.meta_cap * 2);
+    (void) hipHostFree(s.meta_h);
+    (void) hipFree(s.meta_d);
+    s.meta_h = s.meta_d = nullptr;
+    s.meta_cap = 0;
+    hipError_t e = hipHostMalloc(&s.meta_h, need, hipHostMallocDefault);
+    if (e == hipSuccess) {
+        e = hipMalloc(&s.meta_d, need);
+    }
+    if (e == hipSuccess) {
+        s.meta_cap = need;
+    }
+    return e;
+}
+
+// Build group g's plan into slot s (pinned image + device arenas) and return
+// a launchable plan view over the slot's device memory.
+hipError_t stage_plan(PipeSlot &s, const HostGroup &g, DeviceState *st, cio_crc32_plan &view,
+                      uint32_t **d_cid, size_t *meta_bytes, const char **err)
+{
+    const size_t n = g.offs.size();
+    plan_init(&view, st, n);
+    PlanHost ph;
+    if ((*err = plan_build(ph, g.offs.data(), g.lens.data(), n, view.W)) != nullptr) {
+        return hipSuccess;
+    }
+    const size_t o_desc = 0;
+    const size_t o_ws = o_desc + align256(ph.desc.size() * sizeof(ChunkDesc));
+    const size_t o_tiny = o_ws + align256(ph.ws.size() * sizeof(WaveStart));
+    const size_t o_pfac = o_tiny + align256(std::max<size_t>(1, ph.tiny.size()) * sizeof(uint32_t));
+    const size_t o_cid = o_pfac + align256(ph.pfac.size() * sizeof(uint32_t));
+    const size_t total = o_cid + align256(n * sizeof(uint32_t));
+    hipError_t e = grow_meta(s, total);
+    if (e == hipSuccess) e = grow_dev(&s.partials, &s.part_cap, ph.pfac.size(), false, s.stream);
+    if (e == hipSuccess) e = grow_dev(&s.counters, &s.cnt_cap, std::max<size_t>(1, n), true, s.stream);
+    if (e != hipSuccess) {
+        return e;
+    }
+    memcpy(s.meta_h + o_desc, ph.desc.data(), ph.desc.size() * sizeof(ChunkDesc));
+    memcpy(s.meta_h + o_ws, ph.ws.data(), ph.ws.size() * sizeof(WaveStart));
+    if (!ph.tiny.empty()) {
+        memcpy(s.meta_h + o_tiny, ph.tiny.data(), ph.tiny.size() * sizeof(uint32_t));
+    }
+    memcpy(s.meta_h + o_pfac, ph.pfac.data(), ph.pfac.size() * sizeof(uint32_t));
+    memcpy(s.meta_h + o_cid, g.cid.data(), n * sizeof(uint32_t));
+    view.S = ph.S;
+    view.bytes = ph.bytes;
+    view.ntiny = (uint32_t) ph.tiny.size();
+    view.desc = reinterpret_cast<ChunkDesc *>(s.meta_d + o_desc);
+    view.wstart = reinterpret_cast<WaveStart *>(s.meta_d + o_ws);
+    view.tiny = reinterpret_cast<uint32_t *>(s.meta_d + o_tiny);
+    view.pfac = reinterpret_cast<uint32_t *>(s.meta_d + o_pfac);
+    view.partials = s.partials;
+    view.counters = s.counters;
+    *d_cid = reinterpret_cast<uint32_t *>(s.meta_d + o_cid);
+    *meta_bytes = total;
+    return hipSuccess;
 }
 
 }  // namespace
@@ -1258,11 +1535,14 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
     if (!bufs || !lens || !out_raw) {
         return fail("cio_crc32_batch_host: null argument");
     }
+    if (n >= 0xffffffffull) {
+        return fail("cio_crc32_batch_host: too many chunks");
+    }
     DeviceState *st;
     if (device_state(&st) != CIO_OK) {
         return CIO_ERROR;
     }
-    // Build groups of <= kStage bytes, 16-byte aligned segment placement.
+    // Groups of <= kStage bytes, 16-byte aligned segment placement.
     std::vector<HostGroup> groups(1);
     for (size_t i = 0; i < n; i++) {
         const uint8_t *p = reinterpret_cast<const uint8_t *>(bufs[i]);
@@ -1286,76 +1566,70 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
         } while (left > 0);
     }
 
-    int rc = CIO_OK;
-    uint8_t *pinned[2] = {nullptr, nullptr};
-    uint8_t *dbuf[2] = {nullptr, nullptr};
-    uint32_t *d_state = nullptr;
-    hipStream_t stream[2] = {nullptr, nullptr};
-    hipEvent_t copied[2] = {nullptr, nullptr}, done_k[2] = {nullptr, nullptr};
+    HostPipe *hp = nullptr;
+    hipError_t e = pipe_get(&hp);
+    if (e != hipSuccess) {
+        return fail("cio_crc32_batch_host: device", e);
+    }
+    std::lock_guard<std::mutex> lk(hp->mu);
+    if (!hp->ready && (e = pipe_init(*hp)) != hipSuccess) {
+        return fail("cio_crc32_batch_host: pipeline setup", e);
+    }
     std::vector<uint32_t> init(n);
     for (size_t i = 0; i < n; i++) {
         init[i] = seeds ? seeds[i] : 0xffffffffu;
     }
-    hipError_t e = hipSuccess;
-    for (int b = 0; b < 2 && e == hipSuccess; b++) {
-        if ((e = hipHostMalloc(&pinned[b], kStage, hipHostMallocDefault)) != hipSuccess) break;
-        if ((e = hipMalloc(&dbuf[b], kStage + 64)) != hipSuccess) break;
-        if ((e = hipStreamCreateWithFlags(&stream[b], hipStreamNonBlocking)) != hipSuccess) break;
-        if ((e = hipEventCreateWithFlags(&copied[b], hipEventDisableTiming)) != hipSuccess) break;
-        if ((e = hipEventCreateWithFlags(&done_k[b], hipEventDisableTiming)) != hipSuccess) break;
+    PipeSlot &s0 = hp->slot[0];
+    // Every slot is idle between calls (the previous call synchronised them).
+    e = grow_dev(&hp->state, &hp->state_cap, n, false, s0.stream);
+    if (e == hipSuccess) {
+        e = hipMemcpyAsync(hp->state, init.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s0.stream);
     }
-    if (e == hipSuccess) e = hipMalloc(&d_state, n * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemcpy(d_state, init.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        e = hipStreamSynchronize(s0.stream);
+    }
+    int rc = CIO_OK;
+    hipEvent_t prev = nullptr;
     for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
-        HostGroup &g = groups[gi];
-        if (cio_crc32_plan_create(&g.plan, g.offs.data(), g.lens.data(), g.offs.size()) != CIO_OK) {
+        PipeSlot &s = hp->slot[gi % kSlots];
+        const HostGroup &g = groups[gi];
+        if (s.busy) {
+            // The slot's previous group (gi - kSlots) must be fully done.
+            if ((e = hipEventSynchronize(s.done)) != hipSuccess) break;
+            s.busy = false;
+        }
+        cio_crc32_plan view;
+        uint32_t *d_cid = nullptr;
+        size_t meta_bytes = 0;
+        const char *err = nullptr;
+        if ((e = stage_plan(s, g, st, view, &d_cid, &meta_bytes, &err)) != hipSuccess) break;
+        if (err) {
+            rc = fail(err);
+            break;
+        }
+        hp->pool->copy(s.pinned, g);
+        if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
+        if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
+        if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
+        if (plan_exec_impl(&view, s.dbuf, hp->state, hp->state, d_cid, s.stream) != CIO_OK) {
             rc = CIO_ERROR;
             break;
         }
-        if ((e = hipMalloc(&g.d_cid, g.cid.size() * sizeof(uint32_t))) != hipSuccess) break;
-        e = hipMemcpy(g.d_cid, g.cid.data(), g.cid.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if ((e = hipEventRecord(s.done, s.stream)) != hipSuccess) break;
+        s.busy = true;
+        prev = s.done;
     }
-    for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
-        const int b = (int) (gi & 1);
-        HostGroup &g = groups[gi];
-        if (gi >= 2) {
-            // pinned[b] is free once the H2D of group gi-2 has completed.
-            if ((e = hipEventSynchronize(copied[b])) != hipSuccess) break;
+    for (int b = 0; b < kSlots; b++) {
+        PipeSlot &s = hp->slot[b];
+        const hipError_t e2 = hipStreamSynchronize(s.stream);
+        if (e == hipSuccess) {
+            e = e2;
         }
-        parallel_copy(pinned[b], g);
-        if (gi >= 1) {
-            // Chained states: this group's kernels run after the previous group's.
-            if ((e = hipStreamWaitEvent(stream[b], done_k[b ^ 1], 0)) != hipSuccess) break;
-        }
-        if ((e = hipMemcpyAsync(dbuf[b], pinned[b], g.bytes, hipMemcpyHostToDevice, stream[b])) != hipSuccess) break;
-        if ((e = hipEventRecord(copied[b], stream[b])) != hipSuccess) break;
-        if (plan_exec_impl(g.plan, dbuf[b], d_state, d_state, g.d_cid, stream[b]) != CIO_OK) {
-            rc = CIO_ERROR;
-            break;
-        }
-        if ((e = hipEventRecord(done_k[b], stream[b])) != hipSuccess) break;
+        s.busy = false;
     }
     if (e == hipSuccess && rc == CIO_OK) {
-        for (int b = 0; b < 2 && e == hipSuccess; b++) {
-            e = hipStreamSynchronize(stream[b]);
-        }
-        if (e == hipSuccess) {
-            e = hipMemcpy(out_raw, d_state, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
-        }
+        e = hipMemcpy(out_raw, hp->state, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
     }
-    for (auto &g : groups) {
-        cio_crc32_plan_destroy(g.plan);
-        (void) hipFree(g.d_cid);
-    }
-    for (int b = 0; b < 2; b++) {
-        if (stream[b]) (void) hipStreamSynchronize(stream[b]);
-        (void) hipHostFree(pinned[b]);
-        (void) hipFree(dbuf[b]);
-        if (stream[b]) (void) hipStreamDestroy(stream[b]);
-        if (copied[b]) (void) hipEventDestroy(copied[b]);
-        if (done_k[b]) (void) hipEventDestroy(done_k[b]);
-    }
-    (void) hipFree(d_state);
     if (e != hipSuccess) {
         return fail("cio_crc32_batch_host", e);
     }
