@@ -31,6 +31,25 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x)
     return __builtin_bswap32(x);
 }
 
+// gfx950 three-input bit operations (one v_bitop3_b32 each).  The XOR and
+// majority tables are symmetric, so operand order does not matter for them.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+// a ? b : c; table index = (a << 2) | (b << 1) | c (checked by the FIPS 180-4
+// known answers in tests/test_gpu_sha1.py).
+__device__ __forceinline__ uint32_t ch3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xCA);
+}
+
 struct Sha1State {
     uint32_t h0, h1, h2, h3, h4;
 };
@@ -44,21 +63,21 @@ __device__ __forceinline__ void sha1_block(Sha1State &st, uint32_t w[16])
         if (t < 16) {
             wt = w[t];
         } else {
-            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
             w[t & 15] = wt;
         }
         uint32_t f, k;
         if (t < 20) {
-            f = (b & c) | (~b & d);           // Ch
+            f = ch3(b, c, d);                 // Ch
             k = 0x5A827999u;
         } else if (t < 40) {
-            f = b ^ c ^ d;                    // Parity
+            f = xor3(b, c, d);                // Parity
             k = 0x6ED9EBA1u;
         } else if (t < 60) {
-            f = (b & c) | (b & d) | (c & d);  // Maj
+            f = maj3(b, c, d);                // Maj
             k = 0x8F1BBCDCu;
         } else {
-            f = b ^ c ^ d;
+            f = xor3(b, c, d);
             k = 0xCA62C1D6u;
         }
         const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
@@ -85,14 +104,28 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     uint32_t w[16];
     const uint64_t full = len / 64;
     if (((uintptr_t) p & 15u) == 0) {
+        // Aligned: block b+1 is loaded while block b is hashed (one wave per
+        // SIMD here, so nothing else would hide the HBM latency).
         const uint4 *q = reinterpret_cast<const uint4 *>(p);
+        uint4 nx[4];
+        if (full > 0) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                nx[v] = q[v];
+            }
+        }
         for (uint64_t blk = 0; blk < full; ++blk) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                const uint4 x = q[blk * 4 + v];
-                w[4 * v + 0] = bswap32(x.x); w[4 * v + 1] = bswap32(x.y);
-                w[4 * v + 2] = bswap32(x.z); w[4 * v + 3] = bswap32(x.w);
+                w[4 * v + 0] = bswap32(nx[v].x); w[4 * v + 1] = bswap32(nx[v].y);
+                w[4 * v + 2] = bswap32(nx[v].z); w[4 * v + 3] = bswap32(nx[v].w);
             }
+            const uint64_t pf = blk + 1 < full ? blk + 1 : blk;   // clamped: always in bounds
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                nx[v] = q[pf * 4 + v];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the rounds
             sha1_block(st, w);
         }
     } else {
