@@ -57,6 +57,7 @@ constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
 constexpr uint32_t kShiftOff = kSliceBytes;
 constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
+constexpr int kStampWords = 6;              // diagnostic stamps per wave (CIO_GPU_STAMPS)
 
 struct ChunkDesc {
     uint64_t a;        // aligned-down start offset from the batch base
@@ -632,10 +633,15 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
     }
     if (STAMPS && lane == 0) {
         // Diagnostic build only: 100 MHz global clock, per wave.
-        stamps[4 * wave + 0] = t_entry;
-        stamps[4 * wave + 1] = t_tables;
-        stamps[4 * wave + 2] = t_stream;
-        stamps[4 * wave + 3] = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw_id, xcc_id;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+        stamps[kStampWords * wave + 0] = t_entry;
+        stamps[kStampWords * wave + 1] = t_tables;
+        stamps[kStampWords * wave + 2] = t_stream;
+        stamps[kStampWords * wave + 3] = __builtin_amdgcn_s_memrealtime();
+        stamps[kStampWords * wave + 4] = hw_id;    // wave/simd/cu/se placement
+        stamps[kStampWords * wave + 5] = xcc_id;
     }
 }
 
@@ -1009,7 +1015,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
     if (const char *r = getenv("CIO_GPU_STAMPS")) {
-        if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * 4 * sizeof(unsigned long long)) != hipSuccess) {
+        if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * kStampWords * sizeof(unsigned long long)) != hipSuccess) {
             p->stamps = nullptr;
         }
     }
@@ -1041,7 +1047,7 @@ int cioa_debug_stamps(const cio_crc32_plan *p, unsigned long long *host, size_t 
     if (!p || !p->stamps) {
         return 0;
     }
-    const size_t n = std::min(cap, (size_t) p->W * 4);
+    const size_t n = std::min(cap, (size_t) p->W * kStampWords);
     if (hipMemcpy(host, p->stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) {
         return 0;
     }

@@ -52,6 +52,10 @@ def main():
     libs = [load(p) for p in paths]
     for p, lib in zip(paths, libs):
         print(f"{p}: {lib.cio_gpu_version().decode()}", flush=True)
+        if hasattr(lib, "cioa_debug_dispatch_delays"):
+            d = (ctypes.c_float * 8)()
+            lib.cioa_debug_dispatch_delays(d)
+            print("   dispatch delays us by blockIdx%8:", " ".join(f"{x:.2f}" for x in d), flush=True)
     dev = torch.device("cuda:0")
     results = {}
     for cfg in args.cfg.split(","):

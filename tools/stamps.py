@@ -29,9 +29,14 @@ def main():
     for it in range(5):
         plan.exec(buf, out)
         torch.cuda.synchronize()
-        st = np.zeros(4096 * 4 * 2, np.uint64)
+        st = np.zeros(4096 * 6 * 2, np.uint64)
         W = f(plan._handle, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), st.size)
-        t = st[:W * 4].reshape(W, 4).astype(np.int64)
+        raw = st[:W * 6].reshape(W, 6).astype(np.int64)
+        t = raw[:, :4]
+        hw, xcc = raw[:, 4], raw[:, 5]
+        simd = (hw >> 4) & 3
+        print("   simd of wave slot (WG 0..3):", [list(simd.reshape(-1, 16)[b]) for b in range(4)])
+        print("   xcc of WG 0..15:", list((xcc.reshape(-1, 16)[:, 0] & 0xf)[:16]))
         t0 = t[:, 0].min()
         us = (t - t0) / 100.0     # 100 MHz
         q = lambda a: " ".join(f"{np.percentile(a, p):7.2f}" for p in (0, 10, 50, 90, 100))  # noqa: E731
@@ -56,6 +61,16 @@ def main():
         print("   mean finish by wave slot", " ".join(f"{x:5.1f}" for x in wg.mean(0)))
         xcd = np.arange(wg.shape[0]) % 8
         print("   WG max by blockIdx%8   ", " ".join(f"{wg.max(1)[xcd == k].mean():6.1f}" for k in range(8)))
+        # dispatch order: entry and finish by blockIdx // 8 (position within its XCD), 8 bins
+        pos = np.arange(wg.shape[0]) // 8
+        bins = np.array_split(np.arange(pos.max() + 1), 8)
+        print("   WG entry by dispatch pos", " ".join(f"{ent.min(1)[np.isin(pos, b)].mean():6.2f}" for b in bins))
+        print("   WG done by dispatch pos ", " ".join(f"{wg.max(1)[np.isin(pos, b)].mean():6.2f}" for b in bins))
+        print("   corr(entry, done) per WG  %.3f" % np.corrcoef(ent.min(1), wg.max(1))[0, 1])
+        out_dir = os.path.join(ROOT, "gpurun_out")
+        if os.path.isdir(out_dir):
+            np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}.npy"), us)
+            np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}_hw.npy"), raw[:, 4:])
 
 
 if __name__ == "__main__":
