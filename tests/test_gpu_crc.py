@@ -227,3 +227,36 @@ def test_host_batch_end_to_end(cuda, data400):
     assert list(map(int, got)) == want
     got0 = cio.crc32_batch_host(bufs[:1])
     assert int(got0[0]) ^ INIT == 0x103CFA67
+
+
+@pytest.mark.gpu
+def test_host_pipeline_reuse_and_growth(cuda):
+    """The persistent host pipeline across calls whose shapes grow and shrink
+    (plan arenas reallocated, counters re-zeroed, state array regrown)."""
+    rng = np.random.default_rng(11)
+    for count, hi in ((3, 5000), (20000, 4100), (7, 9_000_000), (1, 64), (5000, 20000)):
+        bufs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(0, hi, count)]
+        got = cio.crc32_batch_host(bufs)
+        want = [po.crc_update(INIT, b) for b in bufs]
+        assert list(map(int, got)) == want, (count, hi)
+
+
+@pytest.mark.gpu
+def test_host_pipeline_concurrent_callers(cuda):
+    """Two host threads share the per-device pipeline (serialised by its lock)."""
+    import threading
+    rng = np.random.default_rng(12)
+    jobs = [[rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(1, 400000, 300)]
+            for _ in range(4)]
+    results = [None] * len(jobs)
+
+    def run(k):
+        results[k] = cio.crc32_batch_host(jobs[k])
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for k, bufs in enumerate(jobs):
+        assert list(map(int, results[k])) == [po.crc_update(INIT, b) for b in bufs]
