@@ -57,7 +57,7 @@ constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
 constexpr uint32_t kShiftOff = kSliceBytes;
 constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
-constexpr int kStampWords = 6;              // diagnostic stamps per wave (CIO_GPU_STAMPS)
+constexpr int kStampWords = 8;              // diagnostic stamps per wave (CIO_GPU_STAMPS)
 
 struct ChunkDesc {
     uint64_t a;        // aligned-down start offset from the batch base
@@ -168,14 +168,33 @@ __device__ __forceinline__ uint32_t step_shift(const char *lds, uint32_t lrep, u
            *reinterpret_cast<const uint32_t *>(t + 24576 + (s >> 24) * 32u);
 }
 
-__device__ __forceinline__ uint32_t block16(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
-                                            uint32_t s, const uint4 &v)
+// a ^ b ^ c in one gfx950 v_bitop3_b32.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
-    s = word_step(lds, lb_lo, lb_hi, s, v.x);
-    s = word_step(lds, lb_lo, lb_hi, s, v.y);
-    s = word_step(lds, lb_lo, lb_hi, s, v.z);
-    s = word_step(lds, lb_lo, lb_hi, s, v.w);
-    return s;
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// The steady-state step of one sub-chain: shift(s, 4080) then crc_update over
+// the 16 bytes of v.  The four lookups of every word and the next data word
+// are combined with two 3-input XORs (10 XOR instructions per 16 bytes
+// instead of 19).
+__device__ __forceinline__ uint32_t shift_block16(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
+                                                  uint32_t lrep, uint32_t s, const uint4 &v)
+{
+    const char *t = lds + kShiftOff + lrep;
+    const uint32_t h0 = *reinterpret_cast<const uint32_t *>(t + (s & 0xffu) * 32u);
+    const uint32_t h1 = *reinterpret_cast<const uint32_t *>(t + 8192 + ((s >> 8) & 0xffu) * 32u);
+    const uint32_t h2 = *reinterpret_cast<const uint32_t *>(t + 16384 + ((s >> 16) & 0xffu) * 32u);
+    const uint32_t h3 = *reinterpret_cast<const uint32_t *>(t + 24576 + (s >> 24) * 32u);
+    uint32_t x = xor3(xor3(h0, h1, h2), h3, v.x);
+    const uint32_t w[3] = {v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        x = xor3(xor3(tl<3>(lds, lb_hi, x, 0), tl<2>(lds, lb_hi, x, 1), tl<1>(lds, lb_lo, x, 2)),
+                 tl<0>(lds, lb_lo, x, 3), w[i]);
+    }
+    return xor3(tl<3>(lds, lb_hi, x, 0), tl<2>(lds, lb_hi, x, 1), tl<1>(lds, lb_lo, x, 2)) ^
+           tl<0>(lds, lb_lo, x, 3);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -296,6 +315,24 @@ __device__ __forceinline__ void slow_compute(const char *lds, uint32_t lb_lo, ui
     }
 }
 
+// First step of a chunk on the fast path: zero the h alignment-head bytes
+// and fold the seed into content bytes 0..3 (which may straddle lanes 0 and
+// 1 of sub-chain 0), branch-free.  Same bytes as slow_compute's fix-up.
+__device__ __forceinline__ uint4 head_fix(uint4 v, uint32_t lane, uint32_t h, uint32_t seed)
+{
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int off = (int) (16 * lane) + 4 * i - (int) h;
+        const uint32_t neg = (uint32_t) (-off) & 3u, pos = (uint32_t) off & 3u;
+        const uint32_t keep = off <= -4 ? 0u : (off < 0 ? ~0u << (8 * neg) : ~0u);
+        const uint32_t sx = (off <= -4 || off >= 4) ? 0u
+                          : (off < 0 ? seed << (8 * neg) : seed >> (8 * pos));
+        w[i] = (w[i] & keep) ^ sx;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
 #pragma unroll
@@ -353,35 +390,36 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
     }
 }
 
-template <int D, bool STAMPS = false, int PRIO = 1, int NT = kThreads>
-__global__ void __launch_bounds__(NT, 1)
-crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
+template <bool STAMPS = false, int PRIO = 1, int HB = 2>
+__global__ void __launch_bounds__(kThreads, 1)
+crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
+                    uint32_t W, uint32_t unsteps, uint32_t uh,
+                    const ChunkDesc *__restrict__ desc,
                     const WaveStart *__restrict__ wstart, const uint32_t *__restrict__ tiny,
                     const uint32_t *__restrict__ seeds, uint32_t *out, const uint32_t *__restrict__ cid,
                     unsigned long long *__restrict__ partials, uint32_t *__restrict__ counters,
                     const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
                     const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ pfac,
-                    uint64_t S, uint32_t W, uint32_t n, uint32_t ntiny,
-                    unsigned long long *stamps = nullptr)
+                    uint32_t n, uint32_t ntiny, unsigned long long *stamps = nullptr)
 {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
-    unsigned long long t_entry = 0, t_tables = 0, t_stream = 0;
+    unsigned long long t_entry = 0, t_tables = 0, t_stream = 0, t_first = 0, t_mid = 0;
     if (STAMPS) {
         t_entry = __builtin_amdgcn_s_memrealtime();
     }
 
     // Table entries are computed, not loaded: at kernel start every global
     // load pays cold-cache latency, and the build sits on the critical path.
-    constexpr int kE = 1024 / NT;            // table entries per thread
+    constexpr int kE = 1024 / kThreads;            // table entries per thread
     uint32_t tab_v[kE], tab_sv[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
-        const uint32_t idx = tid + (uint32_t) NT * e;
+        const uint32_t idx = tid + (uint32_t) kThreads * e;
         table_entries(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u, tab_v[e], tab_sv[e]);
     }
 
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (NT / kWave) + (tid >> 6));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
     const uint32_t lane = tid & 63u;
     const uint32_t lb_lo = (lane & 31u) << 2;
     const uint32_t lb_hi = lb_lo | 0x10000u;
@@ -397,10 +435,22 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
     ChunkDesc d = {}, ld = {};
     uint64_t j = 0, lj = 0, nload = 0;
     if (active) {
-        const WaveStart ws = wstart[wave];
-        c = ws.c;
+        if (unsteps) {
+            // Uniform batch (equal lengths, constant 16-byte-multiple stride):
+            // the first chunk and its descriptor follow from the kernel
+            // arguments, so the first loads wait on no memory access.
+            c = (uint32_t) (g0 / unsteps);
+            d.a = ua0 + (uint64_t) c * ustride;
+            d.vlen = uvlen;
+            d.g = (uint64_t) c * unsteps;
+            d.nsteps = unsteps;
+            d.h = uh;
+        } else {
+            const WaveStart ws = wstart[wave];
+            c = ws.c;
+            d = ws.d;
+        }
         c0 = c;
-        d = ws.d;
         j = g0 - d.g;
         lc = c;
         ld = d;
@@ -425,23 +475,30 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
         if (nload > 0) {
             --nload;
             if (++lj == ld.nsteps && nload > 0) {
-                do {
+                if (unsteps) {
                     ++lc;
-                    ld = desc[lc];
-                } while (ld.nsteps == 0);
+                    ld.a += ustride;
+                    ld.g += unsteps;
+                } else {
+                    do {
+                        ++lc;
+                        ld = desc[lc];
+                    } while (ld.nsteps == 0);
+                }
                 lj = 0;
             }
         }
     };
 
-    // The first D steps are requested before the table build so that their
-    // HBM latency overlaps it.
+    // The first HB steps are requested before the table build so that their
+    // HBM latency overlaps it (HB = 2: the second step keeps the memory busy
+    // while the first one is CRC'd, after which one step per wave is in flight).
     // Unconditional (also for inactive waves): a branch here would merge a
     // no-load path into the vmcnt state and make the table build wait for the ring.
-    StepRegs ring[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-        issue(ring[k]);
+    StepRegs cur, pre;
+    issue(cur);
+    if (HB == 2) {
+        issue(pre);
     }
     // Descriptors of the first 64 chunks from c0 (one per lane) for the
     // arrival step at the end; fetched now so that they cost nothing there.
@@ -467,36 +524,36 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
         uint32_t *cshift = cslice + 1024;
 #pragma unroll
         for (int e = 0; e < kE; ++e) {
-            cslice[tid + NT * e] = tab_v[e];
-            cshift[tid + NT * e] = tab_sv[e];
+            cslice[tid + kThreads * e] = tab_v[e];
+            cshift[tid + kThreads * e] = tab_sv[e];
         }
         __syncthreads();
-        constexpr int kSG = 8192 / NT, kHG = 2048 / NT;   // granules per thread
+        constexpr int kSG = 8192 / kThreads, kHG = 2048 / kThreads;   // granules per thread
         uint32_t sv[kSG], hv[kHG];
 #pragma unroll
         for (int i = 0; i < kSG; ++i) {
             // slice image granule g: byte address 16 g -> table pair g >> 12,
             // entry b = (g >> 4) & 255, table half (g >> 3) & 1
-            const uint32_t g = tid + (uint32_t) NT * i;
+            const uint32_t g = tid + (uint32_t) kThreads * i;
             const uint32_t k = 2u * (g >> 12) + ((g >> 3) & 1u);
             sv[i] = cslice[(k << 8) | ((g >> 4) & 255u)];
         }
 #pragma unroll
         for (int i = 0; i < kHG; ++i) {
             // shift image granule g: byte address 16 g = k*8192 + b*32 + replica
-            const uint32_t g = tid + (uint32_t) NT * i;
+            const uint32_t g = tid + (uint32_t) kThreads * i;
             hv[i] = cshift[((g >> 9) << 8) | ((g >> 1) & 255u)];
         }
         __syncthreads();
         uint4 *img = reinterpret_cast<uint4 *>(lds);
 #pragma unroll
         for (int i = 0; i < kSG; ++i) {
-            img[tid + (uint32_t) NT * i] = make_uint4(sv[i], sv[i], sv[i], sv[i]);
+            img[tid + (uint32_t) kThreads * i] = make_uint4(sv[i], sv[i], sv[i], sv[i]);
         }
         uint4 *simg = reinterpret_cast<uint4 *>(lds + kShiftOff);
 #pragma unroll
         for (int i = 0; i < kHG; ++i) {
-            simg[tid + (uint32_t) NT * i] = make_uint4(hv[i], hv[i], hv[i], hv[i]);
+            simg[tid + (uint32_t) kThreads * i] = make_uint4(hv[i], hv[i], hv[i], hv[i]);
         }
     }
     __syncthreads();
@@ -512,13 +569,16 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
         uint64_t g = g0;
 
         // One step: CRC the ring slot (if the wave's range is not exhausted),
-        // publish a piece at a chunk / range end, then refill the slot.
-        auto body = [&](StepRegs &r) {
+        // publish a piece at a chunk / range end.
+        auto crc_step = [&](StepRegs &r) {
             if (g < gend) {
-                if (j != 0 && j < full_end) {
+                if (j < full_end) {
+                    if (j == 0) {
+                        r.q[0] = head_fix(r.q[0], lane, d.h, seed);
+                    }
 #pragma unroll
                     for (int q = 0; q < kSub; ++q) {
-                        s[q] = block16(lds, lb_lo, lb_hi, step_shift(lds, lrep, s[q]), r.q[q]);
+                        s[q] = shift_block16(lds, lb_lo, lb_hi, lrep, s[q], r.q[q]);
                     }
                     const uint64_t e0 = j * kStep + (uint64_t) (lane + 1) * kGran;
 #pragma unroll
@@ -544,10 +604,16 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
                     __hip_atomic_store(&partials[(uint64_t) wave + c], (unsigned long long) contrib,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (g < gend) {
-                        do {
+                        if (unsteps) {
                             ++c;
-                            d = desc[c];
-                        } while (d.nsteps == 0);
+                            d.a += ustride;
+                            d.g += unsteps;
+                        } else {
+                            do {
+                                ++c;
+                                d = desc[c];
+                            } while (d.nsteps == 0);
+                        }
                         j = 0;
 #pragma unroll
                         for (int q = 0; q < kSub; ++q) {
@@ -559,21 +625,40 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
                     }
                 }
             }
-            issue(r);
         };
 
-        // Fixed trip count and a single latch: the loop back edge carries only
-        // the state in which every ring slot was refilled, so the compiler waits
-        // for a slot with vmcnt(4 * (D - 1)) instead of draining the ring.
-        static_assert(D >= 1 && D <= 4, "ring depth");
-        const uint64_t iters = (gend - g0 + D - 1) / D;
-        for (uint64_t it = 0; it < iters; ++it) {
-            if (PRIO) {
-                rotate_prio(slot_group, it);
+        // One step in flight per wave (deeper rings measured slower:
+        // profiles/r01/sweep_ring.txt).  Nothing is requested past the range,
+        // so the wave's last CRC is not followed by a wasted round trip.
+        uint64_t done_head = 0;
+        if (HB == 2) {
+            crc_step(cur);
+            if (nload > 0) {
+                issue(cur);
             }
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                body(ring[k]);
+            crc_step(pre);
+            done_head = 2;
+        }
+        if (STAMPS) {
+            t_first = __builtin_amdgcn_s_memrealtime();     // first steps' data arrived and CRC'd
+        }
+        const uint64_t nsteps_w = gend - g0;
+        const uint64_t iters = nsteps_w > done_head ? nsteps_w - done_head : 0;
+        for (uint64_t it = 0; it < iters; ++it) {
+            if (PRIO == 1) {
+                rotate_prio(slot_group, it);
+            } else if (PRIO >= 2) {
+                // Time-sliced: the 4 waves of a SIMD always hold 4 distinct
+                // levels and each holds every level for equal time (slices of
+                // 2^(10 + PRIO) shader clocks), whatever their progress.
+                rotate_prio(slot_group, __builtin_amdgcn_s_memtime() >> (10 + PRIO));
+            }
+            crc_step(cur);
+            if (nload > 0) {
+                issue(cur);
+            }
+            if (STAMPS && it == iters / 2) {
+                t_mid = __builtin_amdgcn_s_memrealtime();
             }
         }
         if (PRIO) {
@@ -642,6 +727,8 @@ crc32_stream_kernel(const uint8_t *base, const ChunkDesc *__restrict__ desc,
         stamps[kStampWords * wave + 3] = __builtin_amdgcn_s_memrealtime();
         stamps[kStampWords * wave + 4] = hw_id;    // wave/simd/cu/se placement
         stamps[kStampWords * wave + 5] = xcc_id;
+        stamps[kStampWords * wave + 6] = t_first;
+        stamps[kStampWords * wave + 7] = t_mid;
     }
 }
 
@@ -808,7 +895,7 @@ int device_state(DeviceState **out)
 
 }  // namespace
 
-constexpr int kRingDefault = 1;   // steps in flight per wave beyond the one computing (tools/sweep.py: 1 is fastest)
+constexpr int kHeadDefault = 1;   // steps requested before the table build (CIO_GPU_HEAD=1|2)
 
 struct cio_crc32_plan {
     uint32_t n = 0;
@@ -816,9 +903,10 @@ struct cio_crc32_plan {
     uint32_t W = 0;            // waves in the grid
     uint32_t grid = 0;         // workgroups
     uint32_t ntiny = 0;        // chunks with len < 4 (byte-serial)
-    int ring = kRingDefault;   // CIO_GPU_RING=1..4 overrides (tuning)
-    int prio = 1;              // CIO_GPU_PRIO=0 disables the priority rotation
-    int threads = kThreads;    // CIO_GPU_THREADS=512 selects 8-wave workgroups
+    int head = kHeadDefault;   // CIO_GPU_HEAD=1|2 (tuning)
+    int prio = 1;              // CIO_GPU_PRIO: 0 none, 1 per-step rotation, 2/3 time-sliced rotation
+    uint64_t ustride = 0, ua0 = 0, uvlen = 0;   // uniform batch geometry (unsteps > 0)
+    uint32_t unsteps = 0, uh = 0;
     unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     ChunkDesc *desc = nullptr;
@@ -839,7 +927,7 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v3 gfx950 fused-stream ring1 prio-rotate coalesced-nt 4x16B-subchains slice4-lds32x perm";
+    return "chunkio_amd crc32 v4 gfx950 fused-stream head2-ring1 uniform-desc xor3 prio-rotate coalesced-nt 4x16B-subchains slice4-lds32x perm";
 }
 
 int cio_gpu_init(void)
@@ -873,21 +961,14 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     p->st = st;
     p->n = (uint32_t) n;
     if (const char *r = getenv("CIO_GPU_PRIO")) {
-        p->prio = atoi(r) ? 1 : 0;
-    }
-    if (const char *r = getenv("CIO_GPU_RING")) {
         const int v = atoi(r);
-        if (v >= 1 && v <= 3) {
-            p->ring = v;
-        }
+        p->prio = (v >= 0 && v <= 3) ? v : 1;
+    }
+    if (const char *r = getenv("CIO_GPU_HEAD")) {
+        p->head = atoi(r) == 1 ? 1 : 2;
     }
     p->grid = (uint32_t) st->cus;
-    if (const char *r = getenv("CIO_GPU_THREADS")) {
-        if (atoi(r) == 512) {
-            p->threads = 512;
-        }
-    }
-    p->W = p->grid * (p->threads / kWave);
+    p->W = p->grid * (kThreads / kWave);
 }
 
 // Host image of everything a launch reads besides the data.
@@ -987,6 +1068,37 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
     return nullptr;
 }
 
+// Uniform batch: n equal lengths >= 4 at offsets off0 + i * stride with
+// stride a multiple of 16 (every chunk has the same misalignment).  The
+// kernel then derives chunk descriptors arithmetically (CIO_GPU_UNIFORM=0
+// disables).
+void plan_uniform(cio_crc32_plan *p, const uint64_t *offs, const uint64_t *lens, size_t n, const PlanHost &ph)
+{
+    p->unsteps = 0;
+    if (const char *r = getenv("CIO_GPU_UNIFORM")) {
+        if (!atoi(r)) {
+            return;
+        }
+    }
+    if (n == 0 || lens[0] < 4 || ph.desc[0].nsteps == 0) {
+        return;
+    }
+    const uint64_t stride = n > 1 ? offs[1] - offs[0] : 0;
+    if (n > 1 && (offs[1] < offs[0] || (stride & 15) != 0)) {
+        return;
+    }
+    for (size_t i = 1; i < n; i++) {
+        if (lens[i] != lens[0] || offs[i] != offs[0] + i * stride) {
+            return;
+        }
+    }
+    p->ustride = stride;
+    p->ua0 = ph.desc[0].a;
+    p->uvlen = ph.desc[0].vlen;
+    p->uh = ph.desc[0].h;
+    p->unsteps = ph.desc[0].nsteps;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1014,6 +1126,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     p->S = ph.S;
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
+    plan_uniform(p, offs, lens, n, ph);
     if (const char *r = getenv("CIO_GPU_STAMPS")) {
         if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * kStampWords * sizeof(unsigned long long)) != hipSuccess) {
             p->stamps = nullptr;
@@ -1082,27 +1195,26 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 }  // extern "C"
 
-using StreamKernel = decltype(&crc32_stream_kernel<1, false, 1, 1024>);
+using StreamKernel = decltype(&crc32_stream_kernel<false, 1, 2>);
 
-template <int NT>
-static StreamKernel select_ring(int ring, int prio, bool stamps)
+template <int HB>
+static StreamKernel select_prio(int prio, bool stamps)
 {
-    if (stamps) {
-        return prio ? crc32_stream_kernel<1, true, 1, NT> : crc32_stream_kernel<1, true, 0, NT>;
-    }
-    switch (ring * 2 + (prio ? 1 : 0)) {
-    case 2: return crc32_stream_kernel<1, false, 0, NT>;
-    case 4: return crc32_stream_kernel<2, false, 0, NT>;
-    case 5: return crc32_stream_kernel<2, false, 1, NT>;
-    case 6: return crc32_stream_kernel<3, false, 0, NT>;
-    case 7: return crc32_stream_kernel<3, false, 1, NT>;
-    default: return crc32_stream_kernel<1, false, 1, NT>;
+    switch (prio * 2 + (stamps ? 1 : 0)) {
+    case 0: return crc32_stream_kernel<false, 0, HB>;
+    case 1: return crc32_stream_kernel<true, 0, HB>;
+    case 3: return crc32_stream_kernel<true, 1, HB>;
+    case 4: return crc32_stream_kernel<false, 2, HB>;
+    case 5: return crc32_stream_kernel<true, 2, HB>;
+    case 6: return crc32_stream_kernel<false, 3, HB>;
+    case 7: return crc32_stream_kernel<true, 3, HB>;
+    default: return crc32_stream_kernel<false, 1, HB>;
     }
 }
 
-static StreamKernel select_kernel(int ring, int prio, int threads, bool stamps)
+static StreamKernel select_kernel(int head, int prio, bool stamps)
 {
-    return threads == 512 ? select_ring<512>(ring, prio, stamps) : select_ring<1024>(ring, prio, stamps);
+    return head == 1 ? select_prio<1>(prio, stamps) : select_prio<2>(prio, stamps);
 }
 
 // One launch: stream kernel (CRC of every step, per-chunk fold by the last
@@ -1125,11 +1237,12 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
-    auto kern = select_kernel(p->ring, p->prio, p->threads, p->stamps != nullptr);
-    hipLaunchKernelGGL(kern, dim3(p->grid), dim3(p->threads), 0, s,
-                       reinterpret_cast<const uint8_t *>(dev_base), p->desc, p->wstart, p->tiny,
+    auto kern = select_kernel(p->head, p->prio, p->stamps != nullptr);
+    hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
+                       reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
+                       p->W, p->unsteps, p->uh, p->desc, p->wstart, p->tiny,
                        dev_seeds, dev_out, cid, p->partials, p->counters, st->slice, st->shift,
-                       st->x8, p->pfac, p->S, p->W, p->n, p->ntiny, p->stamps);
+                       st->x8, p->pfac, p->n, p->ntiny, p->stamps);
     HIP_TRY(hipGetLastError(), "crc32_stream_kernel launch");
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");

@@ -31,6 +31,7 @@ def load(path):
     lib.cio_gpu_event_create.restype = ctypes.c_void_p
     lib.cio_gpu_event_elapsed_ms.restype = ctypes.c_float
     lib.cio_gpu_event_elapsed_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.cio_gpu_event_record.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.cio_gpu_version.restype = ctypes.c_char_p
     return lib
 
@@ -98,6 +99,7 @@ def main():
             ref = got if ref is None else ref
             assert np.array_equal(got, ref), f"{cfg}: outputs differ"
         times = [[] for _ in libs]
+        times_b2b = [[] for _ in libs]
         for r in range(args.rounds):
             for i, (lib, p, o) in enumerate(zip(libs, plans, outs)):
                 evs = [(lib.cio_gpu_event_create(), lib.cio_gpu_event_create()) for _ in range(args.iters)]
@@ -108,11 +110,22 @@ def main():
                                                    stream, evs[k][0], evs[k][1])
                 torch.cuda.synchronize()
                 us = float(np.mean([lib.cio_gpu_event_elapsed_ms(a, b) for a, b in evs])) * 1e3
+                # back-to-back launches under one event pair (no per-launch events)
+                b0, b1 = lib.cio_gpu_event_create(), lib.cio_gpu_event_create()
+                lib.cio_gpu_event_record(b0, stream)
+                for k in range(args.iters):
+                    lib.cio_crc32_plan_exec(p, bufs[k % nrot].data_ptr(), None, o.data_ptr(), stream)
+                lib.cio_gpu_event_record(b1, stream)
+                torch.cuda.synchronize()
+                us_b2b = lib.cio_gpu_event_elapsed_ms(b0, b1) * 1e3 / args.iters
                 times[i].append(us)
-                print(f"{cfg} round {r} lib{i}: {us:8.2f} us  {total / us / 1e3:8.1f} GB/s", flush=True)
+                times_b2b[i].append(us_b2b)
+                print(f"{cfg} round {r} lib{i}: {us:8.2f} us  {total / us / 1e3:8.1f} GB/s   "
+                      f"back-to-back {us_b2b:8.2f} us/launch", flush=True)
         for i in range(len(libs)):
             med = float(np.median(times[i]))
-            results[f"{cfg}/lib{i}"] = {"us": round(med, 2), "GBps": round(total / med / 1e3, 1)}
+            results[f"{cfg}/lib{i}"] = {"us": round(med, 2), "GBps": round(total / med / 1e3, 1),
+                                        "b2b_us": round(float(np.median(times_b2b[i])), 2)}
         for lib, p in zip(libs, plans):
             lib.cio_crc32_plan_destroy(p)
         del bufs

@@ -19,20 +19,27 @@ def main():
     lens = wl.cfg2_lens() if cfg == "cfg2" else np.full(1024, 4 << 20, np.uint64)
     offs = wl.packed_offsets(lens, align=16)
     dev = torch.device("cuda:0")
-    buf = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=dev)
-    cio.fill_synthetic(buf, offs, lens, 1)
+    # Rotate 4 batches like bench.py, so the 256 MiB Infinity Cache cannot
+    # serve a launch from the previous one.
+    bufs = []
+    for b in range(4):
+        bufs.append(torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=dev))
+        cio.fill_synthetic(bufs[-1], offs, lens, 1 + b)
     out = torch.empty(len(lens), dtype=torch.int32, device=dev)
     plan = cio.Crc32Plan(offs, lens)
     f = cio.lib().cioa_debug_stamps
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
     for it in range(5):
-        plan.exec(buf, out)
+        # 16 back-to-back launches (warm clocks, rotating batches); the stamps
+        # are those of the last one.
+        for k in range(16):
+            plan.exec(bufs[(it + k) % 4], out)
         torch.cuda.synchronize()
-        st = np.zeros(4096 * 6 * 2, np.uint64)
+        st = np.zeros(4096 * 8 * 2, np.uint64)
         W = f(plan._handle, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), st.size)
-        raw = st[:W * 6].reshape(W, 6).astype(np.int64)
-        t = raw[:, :4]
+        raw = st[:W * 8].reshape(W, 8).astype(np.int64)
+        t = np.concatenate([raw[:, :4], raw[:, 6:8]], axis=1)   # entry, tables, stream, exit, first, mid
         hw, xcc = raw[:, 4], raw[:, 5]
         simd = (hw >> 4) & 3
         print("   simd of wave slot (WG 0..3):", [list(simd.reshape(-1, 16)[b]) for b in range(4)])
@@ -43,6 +50,10 @@ def main():
         print(f"{cfg} iter {it}: span {us[:, 3].max():7.2f} us   [pct 0/10/50/90/100]")
         print("   entry      ", q(us[:, 0]))
         print("   tables done", q(us[:, 1]))
+        print("   first step ", q(us[:, 4]))
+        print("   first-tabl ", q(us[:, 4] - us[:, 1]))
+        print("   mid step   ", q(us[:, 5]))
+        print("   1st half   ", q(us[:, 5] - us[:, 4]), " 2nd half", q(us[:, 2] - us[:, 5]))
         print("   stream done", q(us[:, 2]))
         print("   exit       ", q(us[:, 3]))
         print("   stream dur ", q(us[:, 2] - us[:, 1]))
@@ -70,7 +81,7 @@ def main():
         out_dir = os.path.join(ROOT, "gpurun_out")
         if os.path.isdir(out_dir):
             np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}.npy"), us)
-            np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}_hw.npy"), raw[:, 4:])
+            np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}_hw.npy"), raw[:, 4:6])
 
 
 if __name__ == "__main__":
