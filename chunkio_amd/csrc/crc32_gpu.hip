@@ -57,7 +57,8 @@ constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
 constexpr uint32_t kShiftOff = kSliceBytes;
 constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
-constexpr int kStampWords = 8;              // diagnostic stamps per wave (CIO_GPU_STAMPS)
+constexpr int kStampWords = 8;
+              // diagnostic stamps per wave (CIO_GPU_STAMPS)
 
 struct ChunkDesc {
     uint64_t a;        // aligned-down start offset from the batch base
@@ -117,6 +118,44 @@ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b)
         b = (b >> 1) ^ (CIOA_POLY & (0u - (b & 1u)));
     }
     return p;
+}
+
+// b(x) * C(x) mod P for a compile-time C: linear in the 32 bits of b, so the
+// XOR of the images of b's set bits (32 constants, no loop-carried shifts).
+template <uint32_t C>
+struct MulCols {
+    uint32_t v[32];
+    constexpr MulCols() : v{}
+    {
+        for (int j = 0; j < 32; ++j) {
+            v[j] = cx_multmodp(C, 1u << j);
+        }
+    }
+};
+
+template <uint32_t C>
+__device__ __forceinline__ uint32_t mulconst(uint32_t b)
+{
+    constexpr MulCols<C> K;
+    uint32_t p = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        p ^= K.v[j] & (0u - ((b >> j) & 1u));
+    }
+    return p;
+}
+
+// Sub-chain states of a lane whose last step was full, shifted to the lane's
+// row end and XORed: sum_q s_q x^(8 * 1024 (3 - q)), by Horner.
+__device__ __forceinline__ uint32_t fold_full(const uint32_t (&s)[kSub])
+{
+    constexpr uint32_t kXRow = cx_xpow8n(kRow);
+    uint32_t h = s[0];
+#pragma unroll
+    for (int q = 1; q < kSub; ++q) {
+        h = multmodp(kXRow, h) ^ s[q];
+    }
+    return h;
 }
 
 __device__ __forceinline__ uint64_t wave_start(uint64_t w, uint64_t S, uint64_t W)
@@ -390,7 +429,7 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
     }
 }
 
-template <bool STAMPS = false, int PRIO = 1, int HB = 2>
+template <bool STAMPS = false, int PRIO = 1>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
                     uint32_t W, uint32_t unsteps, uint32_t uh,
@@ -430,10 +469,11 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     const bool active = g0 < gend;
 
     // Compute cursor (c, d, j) and load cursor (lc, ld, lj) walk the same
-    // step sequence; the load cursor runs D steps ahead.
+    // step sequence; the load cursor runs one step ahead.
     uint32_t c = 0, lc = 0, c0 = 0;
     ChunkDesc d = {}, ld = {};
-    uint64_t j = 0, lj = 0, nload = 0;
+    uint32_t j = 0, lj = 0;    // step within the chunk (nsteps is 32-bit)
+    uint64_t nload = 0;
     if (active) {
         if (unsteps) {
             // Uniform batch (equal lengths, constant 16-byte-multiple stride):
@@ -451,7 +491,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             d = ws.d;
         }
         c0 = c;
-        j = g0 - d.g;
+        j = (uint32_t) (g0 - d.g);
         lc = c;
         ld = d;
         lj = j;
@@ -490,16 +530,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         }
     };
 
-    // The first HB steps are requested before the table build so that their
-    // HBM latency overlaps it (HB = 2: the second step keeps the memory busy
-    // while the first one is CRC'd, after which one step per wave is in flight).
+    // The first step is requested before the table build so that its HBM
+    // latency overlaps it (requesting two was slower: profiles/r01/ab_v4_steps.txt).
     // Unconditional (also for inactive waves): a branch here would merge a
     // no-load path into the vmcnt state and make the table build wait for the ring.
-    StepRegs cur, pre;
+    StepRegs cur;
     issue(cur);
-    if (HB == 2) {
-        issue(pre);
-    }
     // Descriptors of the first 64 chunks from c0 (one per lane) for the
     // arrival step at the end; fetched now so that they cost nothing there.
     // Clamped, not predicated: a branch would break the ring's vmcnt tracking.
@@ -511,6 +547,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         ar_ns = ad.nsteps;
         ar_np = ad.npieces;
     }
+    // Fold factor of a piece that ends with a full step (the common case):
+    // sub-chain q of lane l then ends 1024 (3 - q) + 16 (63 - l) bytes before
+    // the piece end.  The 1024 (3 - q) parts are compile-time constants
+    // (fold_full); the lane part x^(8 * 16 (63 - l)) is fetched once here
+    // instead of gathered from g_x8 at every piece end.
+    const uint32_t xl = g_x8[kRow - (lane + 1) * kGran];
     // Keep the scheduler from sinking these loads below the table build.
     __builtin_amdgcn_sched_barrier(0);
 
@@ -564,14 +606,15 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     if (active) {
         uint32_t s[kSub] = {0u, 0u, 0u, 0u};
         uint64_t e[kSub] = {0ull, 0ull, 0ull, 0ull};
-        uint64_t full_end = d.vlen / kStep;
+        uint32_t full_end = (uint32_t) (d.vlen / kStep);
         uint32_t seed = (j == 0) ? (seeds ? seeds[cid ? cid[c] : c] : 0xffffffffu) : 0u;
         uint64_t g = g0;
 
-        // One step: CRC the ring slot (if the wave's range is not exhausted),
-        // publish a piece at a chunk / range end.
-        auto crc_step = [&](StepRegs &r) {
-            if (g < gend) {
+        // One step: CRC the ring slot.  Returns true at a piece end (chunk or
+        // range end); the piece is published by piece_end() after the next
+        // step's loads are issued, so their latency overlaps the fold.
+        auto crc_step = [&](StepRegs &r) -> bool {
+            {
                 if (j < full_end) {
                     if (j == 0) {
                         r.q[0] = head_fix(r.q[0], lane, d.h, seed);
@@ -590,19 +633,43 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                 }
                 ++g;
                 ++j;
-                if (j == d.nsteps || g == gend) {
-                    // Piece end: shift every sub-chain state to the piece end,
-                    // reduce over the wave, publish (write-through, agent scope).
-                    const uint64_t pend = min(j * kStep, d.vlen);
-                    uint32_t contrib = 0;
+                return j == d.nsteps || g == gend;
+            }
+        };
+        // Piece end: shift every sub-chain state to the piece end, reduce over
+        // the wave, publish (write-through, agent scope), move to the next chunk.
+        auto piece_end = [&]() {
+            {
+                {
+                    uint32_t contrib;
+                    if (j <= full_end) {
+                        // The last step was full: Horner over the sub-chains
+                        // with the constant x^(8 * 1024), then the lane factor.
+                        // (The asm keeps the compiler from hoisting xl's 32
+                        // bit masks out of the loop into 64 spilled SGPRs.)
+                        uint32_t a = xl;
+                        asm volatile("" : "+v"(a));
+                        contrib = multmodp(a, fold_full(s));
+                    } else {
+                        const uint64_t pend = min(j * kStep, d.vlen);
+                        contrib = 0;
 #pragma unroll
-                    for (int q = 0; q < kSub; ++q) {
-                        const uint64_t dist = e[q] < pend ? pend - e[q] : 0;
-                        contrib ^= s[q] ? multmodp(g_x8[min(dist, (uint64_t) (kX8Count - 1))], s[q]) : 0u;
+                        for (int q = 0; q < kSub; ++q) {
+                            const uint64_t dist = e[q] < pend ? pend - e[q] : 0;
+                            contrib ^= s[q] ? multmodp(g_x8[min(dist, (uint64_t) (kX8Count - 1))], s[q]) : 0u;
+                        }
                     }
                     contrib = wave_xor(contrib);
-                    __hip_atomic_store(&partials[(uint64_t) wave + c], (unsigned long long) contrib,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (d.g >= g0 && j == d.nsteps) {
+                        // The whole chunk lies in this wave's range: the piece
+                        // is the chunk's CRC (no partial slot, no arrival).
+                        if (lane == 0) {
+                            out[cid ? cid[c] : c] = contrib;
+                        }
+                    } else {
+                        __hip_atomic_store(&partials[(uint64_t) wave + c], (unsigned long long) contrib,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                     if (g < gend) {
                         if (unsteps) {
                             ++c;
@@ -620,7 +687,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                             s[q] = 0u;
                             e[q] = 0ull;
                         }
-                        full_end = d.vlen / kStep;
+                        full_end = (uint32_t) (d.vlen / kStep);
                         seed = seeds ? seeds[cid ? cid[c] : c] : 0xffffffffu;
                     }
                 }
@@ -630,20 +697,10 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // One step in flight per wave (deeper rings measured slower:
         // profiles/r01/sweep_ring.txt).  Nothing is requested past the range,
         // so the wave's last CRC is not followed by a wasted round trip.
-        uint64_t done_head = 0;
-        if (HB == 2) {
-            crc_step(cur);
-            if (nload > 0) {
-                issue(cur);
-            }
-            crc_step(pre);
-            done_head = 2;
-        }
         if (STAMPS) {
-            t_first = __builtin_amdgcn_s_memrealtime();     // first steps' data arrived and CRC'd
+            t_first = __builtin_amdgcn_s_memrealtime();
         }
-        const uint64_t nsteps_w = gend - g0;
-        const uint64_t iters = nsteps_w > done_head ? nsteps_w - done_head : 0;
+        const uint64_t iters = gend - g0;
         for (uint64_t it = 0; it < iters; ++it) {
             if (PRIO == 1) {
                 rotate_prio(slot_group, it);
@@ -653,9 +710,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                 // 2^(10 + PRIO) shader clocks), whatever their progress.
                 rotate_prio(slot_group, __builtin_amdgcn_s_memtime() >> (10 + PRIO));
             }
-            crc_step(cur);
+            const bool pe = crc_step(cur);
             if (nload > 0) {
                 issue(cur);
+            }
+            if (pe) {
+                piece_end();
             }
             if (STAMPS && it == iters / 2) {
                 t_mid = __builtin_amdgcn_s_memrealtime();
@@ -673,12 +733,15 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             t_stream = __builtin_amdgcn_s_memrealtime();
         }
         // Lane-parallel: lane i arrives on chunk ac + i when the range holds
-        // a piece of it; the batch of 64 ends the scan if it reaches a
-        // non-empty chunk that starts past the range (or the end of the batch).
+        // a piece of it and the chunk spans more than this range (whole
+        // chunks were written out directly); the batch of 64 ends the scan
+        // if it reaches a non-empty chunk that starts past the range (or the
+        // end of the batch).
         for (uint32_t ac = c0;;) {
             const uint32_t idx = ac + lane;
             const bool inb = idx < n;
-            const bool member = inb && ar_ns != 0 && ar_g < gend;
+            const bool whole = ar_g >= g0 && ar_g + ar_ns <= gend;
+            const bool member = inb && ar_ns != 0 && ar_g < gend && !whole;
             const bool stop = !inb || (ar_ns != 0 && ar_g >= gend);
             uint32_t old = 0;
             if (member) {
@@ -687,8 +750,8 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             for (uint64_t fin = __ballot(member && old + 1 == ar_np); fin; fin &= fin - 1) {
                 const uint32_t b = (uint32_t) __builtin_ctzll(fin);
                 const uint32_t fc = ac + b;
-                const uint64_t fg = ((uint64_t) __builtin_amdgcn_readlane((uint32_t) (ar_g >> 32), b) << 32) |
-                                    __builtin_amdgcn_readlane((uint32_t) ar_g, b);
+                const uint64_t fg = ((uint64_t) (uint32_t) __builtin_amdgcn_readlane((uint32_t) (ar_g >> 32), b) << 32) |
+                                    (uint32_t) __builtin_amdgcn_readlane((uint32_t) ar_g, b);
                 fold_chunk(fg, __builtin_amdgcn_readlane(ar_ns, b), fc, cid ? cid[fc] : fc, lane,
                            partials, pfac, out, counters, S, W);
             }
@@ -895,7 +958,6 @@ int device_state(DeviceState **out)
 
 }  // namespace
 
-constexpr int kHeadDefault = 1;   // steps requested before the table build (CIO_GPU_HEAD=1|2)
 
 struct cio_crc32_plan {
     uint32_t n = 0;
@@ -903,7 +965,6 @@ struct cio_crc32_plan {
     uint32_t W = 0;            // waves in the grid
     uint32_t grid = 0;         // workgroups
     uint32_t ntiny = 0;        // chunks with len < 4 (byte-serial)
-    int head = kHeadDefault;   // CIO_GPU_HEAD=1|2 (tuning)
     int prio = 1;              // CIO_GPU_PRIO: 0 none, 1 per-step rotation, 2/3 time-sliced rotation
     uint64_t ustride = 0, ua0 = 0, uvlen = 0;   // uniform batch geometry (unsteps > 0)
     uint32_t unsteps = 0, uh = 0;
@@ -963,9 +1024,6 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     if (const char *r = getenv("CIO_GPU_PRIO")) {
         const int v = atoi(r);
         p->prio = (v >= 0 && v <= 3) ? v : 1;
-    }
-    if (const char *r = getenv("CIO_GPU_HEAD")) {
-        p->head = atoi(r) == 1 ? 1 : 2;
     }
     p->grid = (uint32_t) st->cus;
     p->W = p->grid * (kThreads / kWave);
@@ -1195,27 +1253,22 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 }  // extern "C"
 
-using StreamKernel = decltype(&crc32_stream_kernel<false, 1, 2>);
+using StreamKernel = decltype(&crc32_stream_kernel<false, 1>);
 
-template <int HB>
-static StreamKernel select_prio(int prio, bool stamps)
+static StreamKernel select_kernel(int prio, bool stamps)
 {
     switch (prio * 2 + (stamps ? 1 : 0)) {
-    case 0: return crc32_stream_kernel<false, 0, HB>;
-    case 1: return crc32_stream_kernel<true, 0, HB>;
-    case 3: return crc32_stream_kernel<true, 1, HB>;
-    case 4: return crc32_stream_kernel<false, 2, HB>;
-    case 5: return crc32_stream_kernel<true, 2, HB>;
-    case 6: return crc32_stream_kernel<false, 3, HB>;
-    case 7: return crc32_stream_kernel<true, 3, HB>;
-    default: return crc32_stream_kernel<false, 1, HB>;
+    case 0: return crc32_stream_kernel<false, 0>;
+    case 1: return crc32_stream_kernel<true, 0>;
+    case 3: return crc32_stream_kernel<true, 1>;
+    case 4: return crc32_stream_kernel<false, 2>;
+    case 5: return crc32_stream_kernel<true, 2>;
+    case 6: return crc32_stream_kernel<false, 3>;
+    case 7: return crc32_stream_kernel<true, 3>;
+    default: return crc32_stream_kernel<false, 1>;
     }
 }
 
-static StreamKernel select_kernel(int head, int prio, bool stamps)
-{
-    return head == 1 ? select_prio<1>(prio, stamps) : select_prio<2>(prio, stamps);
-}
 
 // One launch: stream kernel (CRC of every step, per-chunk fold by the last
 // arriver, tiny chunks).  The per-chunk counters are self-resetting, so no
@@ -1237,7 +1290,7 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
-    auto kern = select_kernel(p->head, p->prio, p->stamps != nullptr);
+    auto kern = select_kernel(p->prio, p->stamps != nullptr);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
                        p->W, p->unsteps, p->uh, p->desc, p->wstart, p->tiny,
