@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident batched CRC-32 on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|sha1|e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg4k|sha1|e2e]
 
 One "step" = one pass of the hot path over one batch: crc_update(init, chunk)
 for every chunk of the batch (main kernel + per-chunk fold), inputs already
@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=200)
-    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "sha1", "e2e"])
+    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     return p.parse_args()
 
@@ -96,6 +96,12 @@ def geometry(cfg, rank, world):
                             "persistent load-balanced kernel", "chunks_per_gpu": int(len(ids)),
                 "bytes_per_gpu": int(lens.sum())}
         return lens, ids, wl.CFG3_SEED, desc, "weak"
+    if cfg == "cfg4k":
+        ids = np.arange(rank, wl.CFG4K_N * world, world, dtype=np.uint64)  # weak: 102400 per GPU
+        lens = np.full(len(ids), wl.CFG4K_LEN, dtype=np.uint64)
+        desc = {"workload": "cfg4k: 102400 x 4096 B chunks per GPU (cfg2's bytes in 4 KiB records), "
+                            "small-chunk kernel", "chunks_per_gpu": int(len(ids)), "chunk_bytes": wl.CFG4K_LEN}
+        return lens, ids, wl.CFG4K_SEED, desc, "weak"
     if cfg == "cfg4":
         ids = wl.shard_round_robin(wl.CFG4_N, rank, world).astype(np.uint64)  # strong: 8192 total
         lens = np.full(len(ids), wl.CFG4_LEN, dtype=np.uint64)
@@ -248,6 +254,9 @@ def run_crc(args, rank, world, device, dist):
             g = json.load(f)["cfg2"]
         check["golden_sha256_match"] = hashlib.sha256(gpu0.astype("<u4").tobytes()).hexdigest() == \
             g["sha256_of_raw_le"]
+    elif args.config == "cfg4k" and rank == 0:
+        from oracle import pyoracle as po
+        check["cpu_oracle_match"] = bool(np.array_equal(po.crc_batch(bufs[0].cpu().numpy(), offs, lens), gpu0))
 
     res = {
         "metric": METRIC if args.config == "cfg2" else f"device-resident CRC32 GB/s ({args.config})",
@@ -260,7 +269,7 @@ def run_crc(args, rank, world, device, dist):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": load_pmc_traffic(args.config),
-                     "kernel": "crc32_stream_kernel", "kernel_ms_mean": round(kernel_ms, 5),
+                     "kernel": plan.kernel_name(), "kernel_ms_mean": round(kernel_ms, 5),
                      "timing": "HIP event pair on the launch stream around the K back-to-back timed "
                                "launches, divided by K (launch gaps included)",
                      "isolated_launch_ms": {"mean": round(float(launch_ms.mean()), 5),

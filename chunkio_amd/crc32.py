@@ -97,6 +97,10 @@ class Crc32Plan:
     def bytes(self):
         return int(_lib.lib().cio_crc32_plan_bytes(self._handle))
 
+    def kernel_name(self):
+        """The kernel this plan launches (crc32_stream_kernel / crc32_small_kernel)."""
+        return _lib.lib().cio_crc32_plan_kernel(self._handle).decode()
+
     def exec(self, base, out, seeds=None, stream=None):
         """base: uint8 cuda tensor; out: int32/uint32 cuda tensor of n; seeds: same or None."""
         _lib.check(_lib.lib().cio_crc32_plan_exec(self._handle, _ptr(base), _ptr(seeds), _ptr(out),

@@ -276,13 +276,64 @@ __device__ __forceinline__ uint32_t basis_entry(uint32_t b)
 
 constexpr uint32_t kXStepShift = cx_xpow8n(kStep - kGran);
 
+// SHIFT = x^(8 d) of the shift table's jump d (kStep - kGran for the stream
+// kernel, kRow - kGran for the small-chunk kernel).
+template <uint32_t SHIFT = kXStepShift>
 __device__ __forceinline__ void table_entries(uint32_t k, uint32_t b, uint32_t &slice, uint32_t &shift)
 {
     switch (k) {
-    case 0: slice = basis_entry<cx_xpow8n(1), 0>(b); shift = basis_entry<kXStepShift, 0>(b); break;
-    case 1: slice = basis_entry<cx_xpow8n(2), 0>(b); shift = basis_entry<kXStepShift, 1>(b); break;
-    case 2: slice = basis_entry<cx_xpow8n(3), 0>(b); shift = basis_entry<kXStepShift, 2>(b); break;
-    default: slice = basis_entry<cx_xpow8n(4), 0>(b); shift = basis_entry<kXStepShift, 3>(b); break;
+    case 0: slice = basis_entry<cx_xpow8n(1), 0>(b); shift = basis_entry<SHIFT, 0>(b); break;
+    case 1: slice = basis_entry<cx_xpow8n(2), 0>(b); shift = basis_entry<SHIFT, 1>(b); break;
+    case 2: slice = basis_entry<cx_xpow8n(3), 0>(b); shift = basis_entry<SHIFT, 2>(b); break;
+    default: slice = basis_entry<cx_xpow8n(4), 0>(b); shift = basis_entry<SHIFT, 3>(b); break;
+    }
+}
+
+// Tables.  Phase 1: thread tid computes entry b = tid & 255 of slice
+// table k = tid >> 8 and of shift table k into compact 4 KiB arrays
+// parked in the shift-table region.  Phase 2: every thread gathers the
+// 10 entries of its granules.  Phase 3: consecutive lanes write
+// consecutive 16-byte granules of the replicated images (bank-conflict
+// free: a thread writing 128 contiguous bytes puts a whole wave on 4 banks).
+constexpr int kE = 1024 / kThreads;            // table entries per thread
+
+__device__ __forceinline__ void write_tables(char *lds, uint32_t tid, const uint32_t (&tab_v)[kE],
+                                             const uint32_t (&tab_sv)[kE])
+{
+    uint32_t *cslice = reinterpret_cast<uint32_t *>(lds + kShiftOff);
+    uint32_t *cshift = cslice + 1024;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        cslice[tid + kThreads * e] = tab_v[e];
+        cshift[tid + kThreads * e] = tab_sv[e];
+    }
+    __syncthreads();
+    constexpr int kSG = 8192 / kThreads, kHG = 2048 / kThreads;   // granules per thread
+    uint32_t sv[kSG], hv[kHG];
+#pragma unroll
+    for (int i = 0; i < kSG; ++i) {
+        // slice image granule g: byte address 16 g -> table pair g >> 12,
+        // entry b = (g >> 4) & 255, table half (g >> 3) & 1
+        const uint32_t g = tid + (uint32_t) kThreads * i;
+        const uint32_t k = 2u * (g >> 12) + ((g >> 3) & 1u);
+        sv[i] = cslice[(k << 8) | ((g >> 4) & 255u)];
+    }
+#pragma unroll
+    for (int i = 0; i < kHG; ++i) {
+        // shift image granule g: byte address 16 g = k*8192 + b*32 + replica
+        const uint32_t g = tid + (uint32_t) kThreads * i;
+        hv[i] = cshift[((g >> 9) << 8) | ((g >> 1) & 255u)];
+    }
+    __syncthreads();
+    uint4 *img = reinterpret_cast<uint4 *>(lds);
+#pragma unroll
+    for (int i = 0; i < kSG; ++i) {
+        img[tid + (uint32_t) kThreads * i] = make_uint4(sv[i], sv[i], sv[i], sv[i]);
+    }
+    uint4 *simg = reinterpret_cast<uint4 *>(lds + kShiftOff);
+#pragma unroll
+    for (int i = 0; i < kHG; ++i) {
+        simg[tid + (uint32_t) kThreads * i] = make_uint4(hv[i], hv[i], hv[i], hv[i]);
     }
 }
 
@@ -408,6 +459,27 @@ __device__ __forceinline__ void fold_chunk(uint64_t g, uint32_t nsteps, uint32_t
     }
 }
 
+// Tiny chunks (len < 4) and empty chunks: byte-serial with the seed, one
+// chunk per lane.
+__device__ __forceinline__ void tiny_chunks(const char *lds, uint32_t lb_lo, const uint8_t *base,
+                                            const ChunkDesc *desc, const uint32_t *tiny,
+                                            const uint32_t *seeds, uint32_t *out, const uint32_t *cid,
+                                            uint32_t ntiny, uint32_t wave, uint32_t lane, uint32_t W)
+{
+    for (uint64_t t = (uint64_t) wave * kWave + lane; t < ntiny; t += (uint64_t) W * kWave) {
+        const uint32_t c = tiny[t];
+        const ChunkDesc d = desc[c];
+        const uint32_t oc = cid ? cid[c] : c;
+        uint32_t st = seeds ? seeds[oc] : 0xffffffffu;
+        const uint8_t *p = base + d.a + d.h;
+        const uint32_t len = (uint32_t) (d.vlen - d.h);
+        for (uint32_t i = 0; i < len; ++i) {
+            st = byte_step(lds, lb_lo, st, p[i]);
+        }
+        out[oc] = st;
+    }
+}
+
 // The CRC kernel: one launch per batch.
 //   1. every workgroup builds the LDS tables (160 KiB);
 //   2. every wave streams its even share of the batch's wave-steps through a
@@ -450,7 +522,6 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 
     // Table entries are computed, not loaded: at kernel start every global
     // load pays cold-cache latency, and the build sits on the critical path.
-    constexpr int kE = 1024 / kThreads;            // table entries per thread
     uint32_t tab_v[kE], tab_sv[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
@@ -556,48 +627,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // Keep the scheduler from sinking these loads below the table build.
     __builtin_amdgcn_sched_barrier(0);
 
-    {   // Tables.  Phase 1: thread tid computes entry b = tid & 255 of slice
-        // table k = tid >> 8 and of shift table k into compact 4 KiB arrays
-        // parked in the shift-table region.  Phase 2: every thread gathers the
-        // 10 entries of its granules.  Phase 3: consecutive lanes write
-        // consecutive 16-byte granules of the replicated images (bank-conflict
-        // free: a thread writing 128 contiguous bytes puts a whole wave on 4 banks).
-        uint32_t *cslice = reinterpret_cast<uint32_t *>(lds + kShiftOff);
-        uint32_t *cshift = cslice + 1024;
-#pragma unroll
-        for (int e = 0; e < kE; ++e) {
-            cslice[tid + kThreads * e] = tab_v[e];
-            cshift[tid + kThreads * e] = tab_sv[e];
-        }
-        __syncthreads();
-        constexpr int kSG = 8192 / kThreads, kHG = 2048 / kThreads;   // granules per thread
-        uint32_t sv[kSG], hv[kHG];
-#pragma unroll
-        for (int i = 0; i < kSG; ++i) {
-            // slice image granule g: byte address 16 g -> table pair g >> 12,
-            // entry b = (g >> 4) & 255, table half (g >> 3) & 1
-            const uint32_t g = tid + (uint32_t) kThreads * i;
-            const uint32_t k = 2u * (g >> 12) + ((g >> 3) & 1u);
-            sv[i] = cslice[(k << 8) | ((g >> 4) & 255u)];
-        }
-#pragma unroll
-        for (int i = 0; i < kHG; ++i) {
-            // shift image granule g: byte address 16 g = k*8192 + b*32 + replica
-            const uint32_t g = tid + (uint32_t) kThreads * i;
-            hv[i] = cshift[((g >> 9) << 8) | ((g >> 1) & 255u)];
-        }
-        __syncthreads();
-        uint4 *img = reinterpret_cast<uint4 *>(lds);
-#pragma unroll
-        for (int i = 0; i < kSG; ++i) {
-            img[tid + (uint32_t) kThreads * i] = make_uint4(sv[i], sv[i], sv[i], sv[i]);
-        }
-        uint4 *simg = reinterpret_cast<uint4 *>(lds + kShiftOff);
-#pragma unroll
-        for (int i = 0; i < kHG; ++i) {
-            simg[tid + (uint32_t) kThreads * i] = make_uint4(hv[i], hv[i], hv[i], hv[i]);
-        }
-    }
+    write_tables(lds, tid, tab_v, tab_sv);
     __syncthreads();
     if (STAMPS) {
         t_tables = __builtin_amdgcn_s_memrealtime();
@@ -766,19 +796,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         }
     }
 
-    // Tiny chunks (len < 4) and empty chunks: byte-serial with the seed.
-    for (uint64_t t = (uint64_t) wave * kWave + lane; t < ntiny; t += (uint64_t) W * kWave) {
-        const uint32_t c = tiny[t];
-        const ChunkDesc d = desc[c];
-        const uint32_t oc = cid ? cid[c] : c;
-        uint32_t st = seeds ? seeds[oc] : 0xffffffffu;
-        const uint8_t *p = base + d.a + d.h;
-        const uint32_t len = (uint32_t) (d.vlen - d.h);
-        for (uint32_t i = 0; i < len; ++i) {
-            st = byte_step(lds, lb_lo, st, p[i]);
-        }
-        out[oc] = st;
-    }
+    tiny_chunks(lds, lb_lo, base, desc, tiny, seeds, out, cid, ntiny, wave, lane, W);
     if (STAMPS && lane == 0) {
         // Diagnostic build only: 100 MHz global clock, per wave.
         uint32_t hw_id, xcc_id;
@@ -793,6 +811,196 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         stamps[kStampWords * wave + 6] = t_first;
         stamps[kStampWords * wave + 7] = t_mid;
     }
+}
+
+// ---------------------------------------------------------------- small chunks
+
+// Batches whose chunks all fit one wave-step (virtual length <= 4096 B, e.g.
+// 4 KiB records).  Every chunk is then its own piece, so the per-chunk fold
+// is what costs: the stream kernel keeps 4 independent sub-chains per lane
+// (1 KiB apart) and pays a Horner pass plus a lane multiply per chunk.  Here
+// the loads are the same coalesced rows (lane l gets bytes 1024 q + 16 l,
+// q = 0..3), but each lane runs ONE chain through its four 16-byte blocks,
+// jumping the 1008 bytes between them with the LDS shift table (built for
+// 1008 instead of 4080).  The chain ends 16 (63 - l) bytes before the chunk
+// end, so the fold is one multiply by x^(8 * 16 (63 - l)) -- a 32 x 32 GF(2)
+// matrix held in registers, 32 masked XORs -- and a wave XOR.
+//
+// A chunk of virtual length v < 4096 is zero-padded to 4096 in registers:
+// the padded CRC is crc * x^(8 (4096 - v)), un-shifted once per chunk by
+// x^(-8 (4096 - v)) (table g_xinv8).  No partial slots, no arrival counters.
+//
+// Chunks are split evenly over the waves by index, output index = chunk
+// index (the host pipeline's chunk-id map uses the stream kernel).  Every
+// ring refill is the same 6 loads (4 data rows, the un-shift factor, the
+// seed), so the compiler's vmcnt waits are exact.
+#ifndef SMALL_EXP
+#define SMALL_EXP 0
+#endif
+struct SmallRegs {
+    uint4 q[kSub];
+    uint32_t inv;    // x^(-8 D), D = 4096 - virtual length
+    uint32_t seed;   // the chunk's seed
+};
+
+// A relaxed load at workgroup scope: a VECTOR load even for a uniform
+// address (an outstanding scalar load would force lgkmcnt(0) on every LDS
+// lookup of the CRC), counted in vmcnt with the ring's data loads.
+__device__ __forceinline__ uint32_t load_vec_u32(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Zero the bytes of a 16-byte block at virtual offset bs past the end v.
+__device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
+{
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t b = bs + 4u * i;
+        const uint32_t nb = b >= vlen ? 0u : min(vlen - b, 4u);    // valid bytes of the word
+        w[i] &= nb >= 4u ? ~0u : ((1u << (8u * nb)) - 1u);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <bool UNI>
+__global__ void __launch_bounds__(kThreads, 1)
+crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t uvlen, uint32_t uh,
+                   uint32_t W, const ChunkDesc *__restrict__ desc, const uint32_t *__restrict__ tiny,
+                   const uint32_t *__restrict__ seeds, uint32_t *out,
+                   const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_xinv8,
+                   uint32_t n, uint32_t ntiny)
+{
+    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+    const uint32_t tid = threadIdx.x;
+    uint32_t tab_v[kE], tab_sv[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t idx = tid + (uint32_t) kThreads * e;
+        table_entries<cx_xpow8n(kRow - kGran)>(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u,
+                                               tab_v[e], tab_sv[e]);
+    }
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
+    const uint32_t lane = tid & 63u;
+    const uint32_t lb_lo = (lane & 31u) << 2;
+    const uint32_t lb_hi = lb_lo | 0x10000u;
+    const uint32_t lrep = (lane & 7u) << 2;
+    const uint32_t c0 = (uint32_t) (((uint64_t) wave * n) / W);
+    const uint32_t c1 = (uint32_t) (((uint64_t) (wave + 1) * n) / W);
+    const uint32_t lbyte = lane * kGran;
+    // Valid dummy address for the optional seeds (the value is discarded).
+    const uint32_t *const seeds_p = seeds ? seeds : g_x8;
+
+    auto geom = [&](uint32_t c, uint64_t &a, uint32_t &vlen, uint32_t &h, bool &live) {
+        if (UNI) {
+            a = ua0 + (uint64_t) c * ustride;
+            vlen = (uint32_t) uvlen;
+            h = uh;
+            // Opaque per chunk: loop-invariant lane masks derived from them
+            // would otherwise be hoisted into (spilled) SGPR pairs.
+            asm volatile("" : "+s"(vlen), "+s"(h));
+            live = true;
+        } else {
+            const ChunkDesc d = desc[c];
+            a = d.a;
+            vlen = (uint32_t) d.vlen;
+            h = d.h;
+            live = d.nsteps != 0;
+        }
+    };
+    // Refill the ring slot with chunk c (past the wave's range: the last
+    // chunk's geometry and the L2-resident g_x8 table as the source).
+    auto issue = [&](SmallRegs &r, uint32_t c) {
+        const bool in = c < c1;
+        const uint32_t cc = in ? c : max(c1, 1u) - 1u;
+        uint64_t a;
+        uint32_t vlen, h;
+        bool live;
+        geom(cc, a, vlen, h, live);
+        const uint32_t last = (max(vlen, 1u) - 1u) & ~15u;
+        const uint8_t *src = in ? base + a : reinterpret_cast<const uint8_t *>(g_x8);
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+            r.q[q] = ldg16(src + min(lbyte + (uint32_t) q * kRow, last));
+        }
+        r.inv = load_vec_u32(g_xinv8 + ((uint32_t) kStep - min(vlen, (uint32_t) kStep)));
+        r.seed = load_vec_u32(seeds_p + (seeds ? cc : 0u));
+    };
+
+    // x^(8 * 16 (63 - l)): the lane's fold factor (requested first: the
+    // register matrix below waits for it).
+    const uint32_t xl = g_x8[kRow - kGran * (lane + 1u)];
+    SmallRegs cur;
+    issue(cur, c0);
+    __builtin_amdgcn_sched_barrier(0);
+    write_tables(lds, tid, tab_v, tab_sv);
+    // The multiply by xl as a 32 x 32 GF(2) matrix held in registers: column
+    // j = xl * x^(31 - j) (reflected bit j).
+    uint32_t col[32];
+    col[31] = xl;
+#pragma unroll
+    for (int j = 30; j >= 0; --j) {
+        col[j] = (col[j + 1] >> 1) ^ (CIOA_POLY & (0u - (col[j + 1] & 1u)));
+    }
+    __syncthreads();
+
+    for (uint32_t c = c0; c < c1; ++c) {
+        uint64_t a;
+        uint32_t vlen, h;
+        bool live;
+        geom(c, a, vlen, h, live);
+        uint32_t st = 0;
+        const uint32_t seed = seeds ? cur.seed : 0xffffffffu;
+        if (live) {
+            StepRegs r;
+#pragma unroll
+            for (int q = 0; q < kSub; ++q) {
+                r.q[q] = cur.q[q];
+            }
+            r.q[0] = head_fix(r.q[0], lane, h, seed);
+            if (vlen < (uint32_t) kStep) {
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    r.q[q] = mask_tail(r.q[q], lbyte + (uint32_t) q * kRow, vlen);
+                }
+            }
+            if (SMALL_EXP & 2) {
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    st ^= r.q[q].x ^ r.q[q].y ^ r.q[q].z ^ r.q[q].w;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    st = shift_block16(lds, lb_lo, lb_hi, lrep, st, r.q[q]);
+                }
+            }
+        }
+        uint32_t inv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(inv) : "v"(cur.inv));
+        // The next chunk's loads go out before the fold.
+        issue(cur, c + 1);
+        if (live) {
+            uint32_t x = st;
+            if (!(SMALL_EXP & 1)) {
+                x = 0;
+#pragma unroll
+                for (int j = 0; j < 32; ++j) {
+                    x ^= col[j] & (0u - ((st >> j) & 1u));
+                }
+            }
+            uint32_t crc = wave_xor(x);
+            if (vlen != (uint32_t) kStep) {
+                asm volatile("" : "+v"(inv));   // (no hoisting of inv's bit masks into SGPRs)
+                crc = multmodp(inv, crc);
+            }
+            if (lane == 0) {
+                out[c] = crc;
+            }
+        }
+    }
+    tiny_chunks(lds, lb_lo, base, desc, tiny, seeds, out, nullptr, ntiny, wave, lane, W);
 }
 
 // ---------------------------------------------------------------- read-only stream
@@ -914,6 +1122,7 @@ struct DeviceState {
     uint32_t *slice = nullptr;   // [4][256] compact
     uint32_t *shift = nullptr;   // [4][256] shift by kStep - kBPL
     uint32_t *x8 = nullptr;      // [kX8Count]
+    uint32_t *xinv8 = nullptr;   // [kStep]: x^(-8 d) (d bytes un-shifted)
 };
 
 std::mutex g_mu;
@@ -950,6 +1159,19 @@ int device_state(DeviceState **out)
         HIP_TRY(hipMemcpy(st.shift, shift, sizeof(shift), hipMemcpyHostToDevice), "upload shift");
         HIP_TRY(hipMemcpy(st.x8, x8.data(), kX8Count * sizeof(uint32_t), hipMemcpyHostToDevice),
                 "upload x8");
+        // x^-1 = (P(x) - 1) / x, reflected: P's low coefficients moved down one power.
+        std::vector<uint32_t> xinv8(kStep);
+        uint32_t xm8 = 0x80000000u;
+        for (int i = 0; i < 8; ++i) {
+            xm8 = cioa_multmodp(xm8, (CIOA_POLY << 1) | 1u);
+        }
+        xinv8[0] = 0x80000000u;
+        for (int d = 1; d < kStep; ++d) {
+            xinv8[d] = cioa_multmodp(xinv8[d - 1], xm8);
+        }
+        HIP_TRY(hipMalloc(&st.xinv8, kStep * sizeof(uint32_t)), "hipMalloc(xinv8)");
+        HIP_TRY(hipMemcpy(st.xinv8, xinv8.data(), kStep * sizeof(uint32_t), hipMemcpyHostToDevice),
+                "upload xinv8");
         st.ready = true;
     }
     *out = &st;
@@ -968,6 +1190,7 @@ struct cio_crc32_plan {
     int prio = 1;              // CIO_GPU_PRIO: 0 none, 1 per-step rotation, 2/3 time-sliced rotation
     uint64_t ustride = 0, ua0 = 0, uvlen = 0;   // uniform batch geometry (unsteps > 0)
     uint32_t unsteps = 0, uh = 0;
+    bool small = false;        // every chunk fits one wave-step: crc32_small_kernel
     unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     ChunkDesc *desc = nullptr;
@@ -1185,6 +1408,12 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
     plan_uniform(p, offs, lens, n, ph);
+    // All chunks within one wave-step (S = number of non-tiny chunks): the
+    // small-chunk kernel (CIO_GPU_SMALL=0 disables).
+    p->small = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
+    if (const char *r = getenv("CIO_GPU_SMALL")) {
+        p->small = p->small && atoi(r) != 0;
+    }
     if (const char *r = getenv("CIO_GPU_STAMPS")) {
         if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * kStampWords * sizeof(unsigned long long)) != hipSuccess) {
             p->stamps = nullptr;
@@ -1228,6 +1457,11 @@ int cioa_debug_stamps(const cio_crc32_plan *p, unsigned long long *host, size_t 
 uint64_t cio_crc32_plan_bytes(const cio_crc32_plan *p)
 {
     return p ? p->bytes : 0;
+}
+
+const char *cio_crc32_plan_kernel(const cio_crc32_plan *p)
+{
+    return (p && p->small) ? "crc32_small_kernel" : "crc32_stream_kernel";
 }
 
 static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const uint32_t *dev_seeds,
@@ -1289,6 +1523,17 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
     const DeviceState *st = p->st;
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
+    }
+    if (p->small && !cid) {
+        auto sk = p->unsteps ? crc32_small_kernel<true> : crc32_small_kernel<false>;
+        hipLaunchKernelGGL(sk, dim3(p->grid), dim3(kThreads), 0, s,
+                           reinterpret_cast<const uint8_t *>(dev_base), p->ustride, p->ua0, p->uvlen, p->uh,
+                           p->W, p->desc, p->tiny, dev_seeds, dev_out, st->x8, st->xinv8, p->n, p->ntiny);
+        HIP_TRY(hipGetLastError(), "crc32_small_kernel launch");
+        if (ev1) {
+            HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");
+        }
+        return CIO_OK;
     }
     auto kern = select_kernel(p->prio, p->stamps != nullptr);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,

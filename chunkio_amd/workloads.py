@@ -20,6 +20,8 @@ GOLDEN = 0x9E3779B97F4A7C15
 CFG2_N, CFG2_LEN, CFG2_SEED = 1024, 409_600, 0xC1000002
 CFG3_N, CFG3_SEED = 65_536, 0xC1000003
 CFG4_N, CFG4_LEN, CFG4_SEED = 8192, 4 * 1024 * 1024, 0xC1000004
+# 4 KiB records (the north star's small-chunk batch): cfg2's bytes in 4 KiB chunks
+CFG4K_N, CFG4K_LEN, CFG4K_SEED = 102_400, 4096, 0xC1000006
 
 
 def splitmix64(x):

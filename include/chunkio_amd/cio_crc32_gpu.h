@@ -103,6 +103,10 @@ int  cio_crc32_plan_exec_events(const cio_crc32_plan *plan, const void *dev_base
 /* Total content bytes the plan covers (sum of lens). */
 uint64_t cio_crc32_plan_bytes(const cio_crc32_plan *plan);
 
+/* Name of the kernel the plan launches: "crc32_stream_kernel" (general
+ * batches) or "crc32_small_kernel" (every chunk within one 4 KiB wave-step). */
+const char *cio_crc32_plan_kernel(const cio_crc32_plan *plan);
+
 /* One-shot: plan + exec + wait + destroy. */
 int  cio_crc32_batch_dev(const void *dev_base, const uint64_t *offs,
                          const uint64_t *lens, const uint32_t *dev_seeds,

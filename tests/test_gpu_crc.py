@@ -123,6 +123,58 @@ def test_more_chunks_than_waves(cuda):
     np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
 
 
+def _uniform(n, ln, stride, mis, seed):
+    """n chunks of ln bytes at mis + i * stride (a uniform batch)."""
+    offs = (mis + np.arange(n, dtype=np.uint64) * np.uint64(stride)).astype(np.uint64)
+    lens = np.full(n, ln, np.uint64)
+    buf = np.zeros(int(offs[-1]) + ln + 64, np.uint8)
+    rng = np.random.default_rng(seed)
+    buf[:] = rng.integers(0, 256, buf.size, dtype=np.uint8)
+    return buf, offs, lens
+
+
+@pytest.mark.parametrize("ln,stride,mis", [
+    (4096, 4096, 0),      # 4 KiB records: the register fold factor path
+    (4090, 4096, 6),      # virtual length 4096 with a 6-byte head (chunk data at map+22 style offsets)
+    (3000, 3008, 0),      # uniform partial step
+    (4, 16, 0),           # smallest chunk that takes the stream path
+    (4096, 4112, 5),      # virtual length 4101: two steps, main kernel
+])
+def test_small_chunk_uniform_batches(cuda, ln, stride, mis):
+    buf, offs, lens = _uniform(9000, ln, stride, mis, seed=ln + mis)
+    want = po.crc_batch(buf, offs, lens)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), want)
+    rng = np.random.default_rng(ln)
+    seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds),
+                                  po.crc_batch(buf, offs, lens, seeds=seeds))
+
+
+def test_small_chunk_mixed_batch_and_kernel_agreement(cuda, monkeypatch):
+    # every chunk within one 4 KiB wave-step (virtual length <= 4096), with
+    # tiny/empty chunks, random misalignment and seeds; the small-chunk kernel
+    # and the stream kernel (CIO_GPU_SMALL=0) must agree with the oracle.
+    rng = np.random.default_rng(11)
+    n = 30000
+    mis = rng.integers(0, 16, n)
+    lens = np.minimum(rng.integers(0, 4097, n), 4096 - mis)
+    lens[::97] = 4096 - mis[::97]                                     # exactly one full step
+    lens[::101] = rng.integers(0, 4, len(lens[::101]))                 # tiny / empty
+    chunks = [wl.gen_chunk(0x5A11, i, int(m)) for i, m in enumerate(lens)]
+    buf, offs, ln = pack(chunks, misalign=mis)
+    seeds = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    want = po.crc_batch(buf, offs, ln, seeds=seeds)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, ln, seeds=seeds), want)
+    monkeypatch.setenv("CIO_GPU_SMALL", "0")
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, ln, seeds=seeds), want)
+
+
+def test_small_chunk_fewer_chunks_than_waves(cuda):
+    for n in (1, 2, 63, 4095, 4097):
+        buf, offs, lens = _uniform(n, 4096, 4096, 0, seed=n)
+        np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
+
+
 def test_one_huge_chunk_spans_all_waves(cuda):
     n = 48 * 1024 * 1024 + 12345
     data = wl.gen_chunk(0xBEEF, 0, n)

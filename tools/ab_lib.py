@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--cfg", default="cfg2,big")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the output equality check")
     args = ap.parse_args()
     import torch
     import chunkio_amd as cio
@@ -97,7 +98,7 @@ def main():
             torch.cuda.synchronize()
             got = o.cpu().numpy().copy()
             ref = got if ref is None else ref
-            assert np.array_equal(got, ref), f"{cfg}: outputs differ"
+            assert args.no_check or np.array_equal(got, ref), f"{cfg}: outputs differ"
         times = [[] for _ in libs]
         times_b2b = [[] for _ in libs]
         for r in range(args.rounds):
