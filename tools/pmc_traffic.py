@@ -16,7 +16,11 @@ import json
 import os
 import sys
 
-KERNEL = "crc32_stream_kernel"
+# the CRC kernel a bench config launches (one of the two per run)
+KERNELS = ("crc32_stream_kernel", "crc32_small_kernel")
+
+
+kern_seen = set()
 
 
 def per_dispatch(d, counter):
@@ -24,8 +28,10 @@ def per_dispatch(d, counter):
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if KERNEL not in row.get("Kernel_Name", ""):
+                name = row.get("Kernel_Name", "")
+                if not any(k in name for k in KERNELS):
                     continue
+                kern_seen.add(next(k for k in KERNELS if k in name))
                 if row.get("Counter_Name") != counter:
                     continue
                 key = row.get("Dispatch_Id") or row.get("Correlation_Id")
@@ -40,12 +46,12 @@ def main():
     fetch = per_dispatch(fdir, "FETCH_SIZE")
     write = per_dispatch(wdir, "WRITE_SIZE")
     if not fetch:
-        sys.exit("no FETCH_SIZE rows for " + KERNEL)
+        sys.exit("no FETCH_SIZE rows for " + "/".join(KERNELS))
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write) if write else 0.0
     read_b = 2.0 * f_kib * 1024.0          # gfx950 correction: FETCH_SIZE = 1/2 of streamed bytes
     write_b = w_kib * 1024.0
-    out = {"kernel": KERNEL, "dispatches": len(fetch),
+    out = {"kernel": "/".join(sorted(kern_seen)), "dispatches": len(fetch),
            "fetch_size_kib_raw": round(f_kib, 1), "write_size_kib_raw": round(w_kib, 1),
            "read_bytes_per_launch": int(read_b), "write_bytes_per_launch": int(write_b),
            "hbm_bytes_per_launch": int(read_b + write_b), "algorithmic_bytes_per_launch": algo,
