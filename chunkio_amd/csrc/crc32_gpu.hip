@@ -837,6 +837,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 #ifndef SMALL_EXP
 #define SMALL_EXP 0
 #endif
+#ifndef SMALL_SLOTS
+#define SMALL_SLOTS 1            // chunks in flight per wave (A/B knob)
+#endif
 struct SmallRegs {
     uint4 q[kSub];
     uint32_t inv;    // x^(-8 D), D = 4096 - virtual length
@@ -931,8 +934,14 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     // x^(8 * 16 (63 - l)): the lane's fold factor (requested first: the
     // register matrix below waits for it).
     const uint32_t xl = g_x8[kRow - kGran * (lane + 1u)];
+#if SMALL_SLOTS == 2
+    SmallRegs ra, rb;
+    issue(ra, c0);
+    issue(rb, c0 + 1);
+#else
     SmallRegs cur;
     issue(cur, c0);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     write_tables(lds, tid, tab_v, tab_sv);
     // The multiply by xl as a 32 x 32 GF(2) matrix held in registers: column
@@ -945,11 +954,12 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     }
     __syncthreads();
 
-    for (uint32_t c = c0; c < c1; ++c) {
+    auto chunk = [&](SmallRegs &cur, uint32_t c) {
         uint64_t a;
         uint32_t vlen, h;
         bool live;
-        geom(c, a, vlen, h, live);
+        geom(c < c1 ? c : max(c1, 1u) - 1u, a, vlen, h, live);
+        live = live && c < c1;
         uint32_t st = 0;
         const uint32_t seed = seeds ? cur.seed : 0xffffffffu;
         if (live) {
@@ -980,7 +990,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         uint32_t inv;
         asm volatile("v_mov_b32 %0, %1" : "=v"(inv) : "v"(cur.inv));
         // The next chunk's loads go out before the fold.
-        issue(cur, c + 1);
+        issue(cur, c + SMALL_SLOTS);
         if (live) {
             uint32_t x = st;
             if (!(SMALL_EXP & 1)) {
@@ -999,7 +1009,17 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
                 out[c] = crc;
             }
         }
+    };
+#if SMALL_SLOTS == 2
+    for (uint32_t c = c0; c < c1; c += 2) {
+        chunk(ra, c);
+        chunk(rb, c + 1);
     }
+#else
+    for (uint32_t c = c0; c < c1; ++c) {
+        chunk(cur, c);
+    }
+#endif
     tiny_chunks(lds, lb_lo, base, desc, tiny, seeds, out, nullptr, ntiny, wave, lane, W);
 }
 
