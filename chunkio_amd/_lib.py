@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libchunkio_amd.so")
+# CIO_AMD_LIB: alternate build of the same ABI (A/B measurements only).
+LIB_PATH = os.environ.get("CIO_AMD_LIB") or os.path.join(HERE, "lib", "libchunkio_amd.so")
 
 # Every symbol the public headers declare (checked by tests/test_abi.py).
 EXPORTS = (
@@ -61,6 +62,8 @@ def _bind(lib):
         "cio_gpu_stream_sync": (ctypes.c_int, [V]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("CIO_AMD_LIB") and not hasattr(lib, name):
+            continue   # an older A/B build without this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

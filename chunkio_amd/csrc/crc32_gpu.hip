@@ -14,17 +14,18 @@
 //   4 KiB wave-steps; step j of a chunk covers virtual bytes [4096 j, 4096 j
 //   + 4096) where the virtual chunk is the content prefixed by its (off & 15)
 //   misalignment bytes, which are zeroed (a zero-seeded CRC ignores leading
-//   zeros) so every load is an aligned 16-byte global_load_dwordx4.  Lane l of
-//   a wave owns the 64 contiguous bytes [64 l, 64 l + 64) of a step and runs
-//   a slice-by-4 chain over them with lookup tables held in LDS, replicated
-//   32 times so lane l always hits bank (l & 31): no data-dependent bank
-//   conflicts.  Between two steps a lane's state jumps over the 4032 bytes of
-//   the other 63 lanes (one 4-lookup shift table).  The seed is folded into
-//   the first 4 content bytes.  At the end of a piece (the steps of one chunk
-//   that one wave owns) each lane shifts its state to the piece end
-//   (x^(8d) table + GF(2) multiply) and the wave XOR-reduces with __shfl_xor.
-//   A small second kernel folds a chunk's pieces in order (Horner with
-//   x^(8 bytes)) -> one raw CRC per chunk.
+//   zeros) so every load is an aligned 16-byte global_load_dwordx4.  A step
+//   is 4 coalesced 1 KiB rows; lane l runs 4 sub-chains, sub-chain q over the
+//   16 bytes [1024 q + 16 l, +16) of every step, slice-by-4 with lookup tables
+//   held in LDS, replicated 32 times so lane l always hits bank (l & 31): no
+//   data-dependent bank conflicts.  Between two steps a sub-chain jumps the
+//   4080 bytes to its next block (one 4-lookup shift table).  The seed is
+//   folded into the first 4 content bytes.  At the end of a piece (the steps
+//   of one chunk that one wave owns) the sub-chains are shifted to the piece
+//   end (Horner over q + one lane factor) and the wave XOR-reduces with
+//   __shfl_xor.  A whole-chunk piece is the chunk's CRC; otherwise the last
+//   wave to publish a piece of the chunk folds the pieces -> one raw CRC per
+//   chunk.  Batches of chunks <= 4 KiB use crc32_small_kernel instead.
 //
 //   Work partition: the S wave-steps of the whole batch are split evenly over
 //   the W persistent waves of the grid (one 1024-thread workgroup per CU), so
@@ -1231,7 +1232,7 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v4 gfx950 fused-stream head2-ring1 uniform-desc xor3 prio-rotate coalesced-nt 4x16B-subchains slice4-lds32x perm";
+    return "chunkio_amd crc32 v5 gfx950 fused-stream ring1 uniform-desc xor3 prio-rotate coalesced-nt 4x16B-subchains slice4-lds32x perm horner-fold direct-whole small-chunk-kernel";
 }
 
 int cio_gpu_init(void)
