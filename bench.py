@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident batched CRC-32 on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg4k|sha1|e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg4k|sha1|e2e|perf]
 
 One "step" = one pass of the hot path over one batch: crc_update(init, chunk)
 for every chunk of the batch (main kernel + per-chunk fold), inputs already
@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=200)
-    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e"])
+    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e", "perf"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     return p.parse_args()
 
@@ -374,6 +374,80 @@ def e2e_breakdown(host, device):
             "torch_threads": torch.get_num_threads()}
 
 
+def run_perf(args, rank, world, device, dist):
+    """BASELINE config 1's loop (`tools/cio -k -p 400kb.txt`: 1000 files x 5 x
+    409600 B with CRC32) with the CRC deferred off the append path and the
+    chunks synced in batches of 100 through ONE GPU pass each
+    (cio_file_sync_batch).  Host-memory end to end; Python chunk layer
+    (chunkio_amd/chunkfile.py), files on the box's /tmp.  The reference loop
+    (oracle/_ref: the reference's own crc_update under the restated loop) is
+    timed beside it, with and without the CRC."""
+    import ctypes
+    import shutil
+    from chunkio_amd import chunkfile as cf
+    d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8).tobytes()
+    files, writes, batch = 1000, 5, 100
+    reps = max(1, min(args.steps, 3))
+
+    def one_pass(path):
+        for b0 in range(0, files, batch):
+            group = []
+            for i in range(b0, b0 + batch):
+                c, _ = cf.ChunkFile.open(os.path.join(path, f"perf-test-{i:04d}.txt"), deferred_crc=True)
+                for _ in range(writes):
+                    c.write(d400)
+                group.append(c)
+            cf.sync_batch(group)
+            for c in group:
+                c.close()
+
+    root = tempfile.mkdtemp(prefix="cioa-perf-gpu-")
+    try:
+        warm = os.path.join(root, "warm")
+        os.makedirs(warm)
+        one_pass(warm)                     # first GPU/pipeline use, page cache
+        shutil.rmtree(warm)
+        times = []
+        for r in range(reps):
+            path = os.path.join(root, f"run{r}")
+            os.makedirs(path)
+            t0 = time.perf_counter()
+            one_pass(path)
+            times.append(time.perf_counter() - t0)
+            with open(os.path.join(path, "perf-test-0999.txt"), "rb") as f:
+                hdr_ok = f.read(10).hex() == "c100088740e700000000"
+            shutil.rmtree(path)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    nbytes = files * writes * len(d400)
+    t = min(times)
+    from oracle import pyoracle as po
+    lib = po.ref()
+    kind, prefix = "reference", "ref_"
+    if lib is None:
+        lib, kind, prefix = po.oracle(), "port", "oracle_"
+    buf = np.frombuffer(d400, np.uint8)
+    ref = {}
+    for ck in (1, 0):
+        with tempfile.TemporaryDirectory(prefix="cioa-perf-") as tmp:
+            nb = ctypes.c_uint64(0)
+            secs = getattr(lib, prefix + "cio_perf_write")(tmp.encode(), buf.ctypes.data, buf.size,
+                                                           files, writes, ck, ctypes.byref(nb))
+            ref["crc_on" if ck else "crc_off"] = {"seconds": round(secs, 4),
+                                                   "GBps": round(nb.value / secs / 1e9, 3)}
+    return {"metric": "cio -k -p loop (1000 files x 5 x 400 KB, CRC32) GB/s with deferred CRC + batched GPU sync",
+            "value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": reps, "warmup": 1,
+            "ms_per_step": round(t * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "tests/golden/400kb.txt (the reference's perf input)",
+            "config": {"workload": "config 1 loop: open, 5 x write 409600 B, sync (batches of 100 chunks "
+                                   "per GPU pass), close; Python chunk layer", "files": files,
+                       "writes": writes, "sync_batch": batch},
+            "check": {"last_file_header_c100088740e7": bool(hdr_ok)},
+            "cpu_baseline": {"value": ref["crc_on"]["GBps"], "unit": "GB/s", "cores": 1, "kind": kind,
+                             "sample": "the same loop in C with crc_update per write (1 thread)",
+                             "crc_off_GBps": ref["crc_off"]["GBps"]}}
+
+
 def main():
     args = parse()
     rank, world, device, dist = dist_setup(args)
@@ -381,6 +455,8 @@ def main():
         res = run_sha1(args, rank, world, device, dist)
     elif args.config == "e2e":
         res = run_e2e(args, rank, world, device, dist)
+    elif args.config == "perf":
+        res = run_perf(args, rank, world, device, dist)
     else:
         res = run_crc(args, rank, world, device, dist)
     if rank == 0:

@@ -25,6 +25,8 @@ EXPORTS = (
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
     # include/chunkio_amd/cio_verify.h
     "cio_file_verify_batch", "cio_verify_paths",
+    # include/chunkio_amd/cio_sync.h
+    "cio_file_sync_batch",
 )
 
 _lib = None

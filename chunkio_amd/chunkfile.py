@@ -23,6 +23,13 @@ the reference does at src/cio_file.c:110.
 
 verify_paths(paths) is the batched verify-on-load of a stream directory
 (cio_scan_stream_files, src/cio_scan.c:39-125) in one GPU pass.
+
+ChunkFile(..., deferred_crc=True) takes the CRC off the append path: write()
+only copies (no crc_update, no raw state at map+2) and sync_batch(files)
+brings every dirty chunk's CRC up to date in one GPU pass seeded with its
+crc_cur (cio_file_sync_batch, include/chunkio_amd/cio_sync.h).  After the sync
+the file bytes are identical to the reference's write/sync sequence; between
+a write and the sync, map+2 (cio_file_hash) still holds the previous header.
 """
 import ctypes
 import mmap
@@ -38,6 +45,7 @@ CIO_OK, CIO_ERROR, CIO_RETRY, CIO_CORRUPTED = 0, -1, -2, -3
 CIO_OPEN, CIO_OPEN_RD, CIO_CHECKSUM = 1, 2, 4
 CIO_ERR_BAD_CHECKSUM, CIO_ERR_BAD_LAYOUT, CIO_ERR_PERMISSION, CIO_ERR_BAD_FILE_SIZE = -10, -11, -12, -13
 CIOA_VERIFY_WRITEBACK = 64
+CIOA_SYNC_FINALIZE, CIOA_SYNC_MSYNC = 1, 2
 
 HDR_MIN = 24
 CONTENT_OFFSET = 22
@@ -58,6 +66,11 @@ class VerifyItem(ctypes.Structure):
                 ("meta_len", ctypes.c_uint16), ("content_len", ctypes.c_uint64)]
 
 
+class SyncItem(ctypes.Structure):
+    _fields_ = [("map", ctypes.c_void_p), ("fs_size", ctypes.c_size_t), ("crc_end", ctypes.c_uint64),
+                ("crc_cur", ctypes.c_uint32), ("status", ctypes.c_int)]
+
+
 def _bind():
     lib = _lib.lib()
     if not hasattr(lib, "_verify_bound"):
@@ -67,6 +80,8 @@ def _bind():
         lib.cio_verify_paths.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                          ctypes.POINTER(ctypes.c_uint32)]
+        lib.cio_file_sync_batch.restype = ctypes.c_int
+        lib.cio_file_sync_batch.argtypes = [ctypes.POINTER(SyncItem), ctypes.c_size_t, ctypes.c_int]
         lib._verify_bound = True
     return lib
 
@@ -86,12 +101,47 @@ def verify_paths(paths, flags=CIO_CHECKSUM):
     return st[:n], er[:n], cr[:n]
 
 
+def sync_batch(files):
+    """Sync many chunk files at once: the deferred-CRC ones through ONE GPU
+    batch (cio_file_sync_batch, finalize + msync), the others one by one."""
+    dirty = [f for f in files if f.map is not None and not f.synced and (f.flags & CIO_OPEN)]
+    batch = [f for f in dirty if f.deferred_crc and (f.flags & CIO_CHECKSUM)]
+    for f in dirty:
+        if f not in batch:
+            f.sync()
+    if not batch:
+        return CIO_OK
+    items = (SyncItem * len(batch))()
+    views = []
+    for it, f in zip(items, batch):
+        v = (ctypes.c_char * f.alloc_size).from_buffer(f.map)
+        views.append(v)
+        it.map = ctypes.addressof(v)
+        it.fs_size = f.alloc_size
+        it.crc_end = f.crc_end
+        it.crc_cur = f.crc_cur
+    rc = _bind().cio_file_sync_batch(items, len(batch), CIOA_SYNC_FINALIZE | CIOA_SYNC_MSYNC)
+    del views
+    _lib.check(rc, "cio_file_sync_batch")
+    for it, f in zip(items, batch):
+        if it.status != CIO_OK:
+            f.error = CIO_ERR_BAD_LAYOUT
+            continue
+        f.crc_cur = int(it.crc_cur)
+        f.crc_end = int(it.crc_end)
+        f.synced = True
+        f.fs_size = os.fstat(f.fd).st_size
+    return CIO_OK
+
+
 class ChunkFile:
     """One filesystem chunk with the reference's layout and CRC semantics."""
 
-    def __init__(self, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None):
+    def __init__(self, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None, deferred_crc=False):
         self.path = path
         self.flags = flags
+        self.deferred_crc = deferred_crc
+        self.crc_end = CONTENT_OFFSET     # file offset up to which crc_cur is current
         self.realloc_size = realloc_size or PAGE * 8
         self.fd = -1
         self.map = None
@@ -106,8 +156,8 @@ class ChunkFile:
 
     # -- open / map -------------------------------------------------------
     @classmethod
-    def open(cls, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None):
-        cf = cls(path, flags, realloc_size)
+    def open(cls, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None, deferred_crc=False):
+        cf = cls(path, flags, realloc_size, deferred_crc)
         rc = cf.up()
         if rc != CIO_OK:
             cf._close_fd()
@@ -138,6 +188,7 @@ class ChunkFile:
             self.synced = False
             if self.flags & CIO_CHECKSUM:
                 self.crc_cur = crc_update(CRC_INIT, self.map[CONTENT_OFFSET:CONTENT_OFFSET + 2])
+                self.crc_end = HDR_MIN
             return CIO_OK
         prot = mmap.PROT_READ | (mmap.PROT_WRITE if rw else 0)
         self.map = mmap.mmap(self.fd, fs_size, prot=prot)
@@ -168,6 +219,7 @@ class ChunkFile:
         self.data_size = int(item[0].content_len)
         if self.flags & CIO_CHECKSUM:
             self.crc_cur = int(item[0].crc_raw)
+            self.crc_end = HDR_MIN + self.meta_len() + self.data_size
         return CIO_OK
 
     def down(self):
@@ -235,12 +287,17 @@ class ChunkFile:
             self._resize(_round_up(new_size, PAGE))
         if self.crc_reset:
             self._set_content_len(self.data_size)
-        if self.flags & CIO_CHECKSUM:
+        if self.flags & CIO_CHECKSUM and self.deferred_crc:
+            if self.crc_reset:                       # full recompute at the sync
+                self.crc_cur, self.crc_end = CRC_INIT, CONTENT_OFFSET
+                self.crc_reset = False
+        elif self.flags & CIO_CHECKSUM:
             if self.crc_reset:                       # update_checksum (:103-108)
                 self.crc_cur = self._region_crc()
                 self.crc_reset = False
             self.crc_cur = crc_update(self.crc_cur, data)
             self.map[2:10] = struct.pack("<Q", self.crc_cur)   # raw 8-byte crc_t (:111)
+            self.crc_end = HDR_MIN + meta + self.data_size + len(data)
         off = HDR_MIN + meta + self.data_size
         self.map[off:off + len(data)] = data
         self.data_size += len(data)
@@ -266,8 +323,11 @@ class ChunkFile:
         self.map[HDR_MIN:HDR_MIN + len(meta)] = meta
         self.map[HDR_MIN + len(meta):HDR_MIN + len(meta) + self.data_size] = content
         self.map[CONTENT_OFFSET:CONTENT_OFFSET + 2] = struct.pack(">H", len(meta))
-        if self.flags & CIO_CHECKSUM:
+        if self.flags & CIO_CHECKSUM and self.deferred_crc:
+            self.crc_cur, self.crc_end = CRC_INIT, CONTENT_OFFSET
+        elif self.flags & CIO_CHECKSUM:
             self.crc_cur = self._region_crc()
+            self.crc_end = HDR_MIN + len(meta) + self.data_size
         self.synced = False
         return 0
 
@@ -275,6 +335,8 @@ class ChunkFile:
         """cio_file_sync (src/cio_file.c:1147-1250) without trimming."""
         if self.map is None or self.synced or not (self.flags & CIO_OPEN):
             return 0
+        if self.deferred_crc and self.flags & CIO_CHECKSUM:
+            return sync_batch([self])
         if self.flags & CIO_CHECKSUM:
             fin = (self.crc_cur ^ 0xFFFFFFFF) & 0xFFFFFFFF
             self.map[2:10] = struct.pack("<Q", int.from_bytes(struct.pack(">I", fin), "little"))
