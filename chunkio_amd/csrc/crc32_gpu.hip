@@ -833,8 +833,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 //
 // Chunks are split evenly over the waves by index, output index = chunk
 // index (the host pipeline's chunk-id map uses the stream kernel).  Every
-// ring refill is the same 6 loads (4 data rows, the un-shift factor, the
-// seed), so the compiler's vmcnt waits are exact.
+// ring refill is the same loads (4 data rows; the un-shift factor unless the
+// batch is uniform; the seed when seeds are given), so the compiler's vmcnt
+// waits are exact.
 #ifndef SMALL_EXP
 #define SMALL_EXP 0
 #endif
@@ -868,7 +869,7 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <bool UNI>
+template <bool UNI, bool SEEDS>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t uvlen, uint32_t uh,
                    uint32_t W, const ChunkDesc *__restrict__ desc, const uint32_t *__restrict__ tiny,
@@ -928,13 +929,19 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         for (int q = 0; q < kSub; ++q) {
             r.q[q] = ldg16(src + min(lbyte + (uint32_t) q * kRow, last));
         }
-        r.inv = load_vec_u32(g_xinv8 + ((uint32_t) kStep - min(vlen, (uint32_t) kStep)));
-        r.seed = load_vec_u32(seeds_p + (seeds ? cc : 0u));
+        if (!UNI) {
+            r.inv = load_vec_u32(g_xinv8 + ((uint32_t) kStep - min(vlen, (uint32_t) kStep)));
+        }
+        if (SEEDS) {
+            r.seed = load_vec_u32(seeds_p + cc);
+        }
     };
 
     // x^(8 * 16 (63 - l)): the lane's fold factor (requested first: the
     // register matrix below waits for it).
     const uint32_t xl = g_x8[kRow - kGran * (lane + 1u)];
+    // Uniform batch: one un-shift factor for every chunk.
+    const uint32_t inv_u = UNI ? g_xinv8[(uint32_t) kStep - min((uint32_t) uvlen, (uint32_t) kStep)] : 0u;
 #if SMALL_SLOTS == 2
     SmallRegs ra, rb;
     issue(ra, c0);
@@ -962,7 +969,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         geom(c < c1 ? c : max(c1, 1u) - 1u, a, vlen, h, live);
         live = live && c < c1;
         uint32_t st = 0;
-        const uint32_t seed = seeds ? cur.seed : 0xffffffffu;
+        const uint32_t seed = SEEDS ? cur.seed : 0xffffffffu;
         if (live) {
             StepRegs r;
 #pragma unroll
@@ -988,8 +995,10 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
                 }
             }
         }
-        uint32_t inv;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(inv) : "v"(cur.inv));
+        uint32_t inv = inv_u;
+        if (!UNI) {
+            asm volatile("v_mov_b32 %0, %1" : "=v"(inv) : "v"(cur.inv));
+        }
         // The next chunk's loads go out before the fold.
         issue(cur, c + SMALL_SLOTS);
         if (live) {
@@ -1546,7 +1555,8 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
     if (p->small && !cid) {
-        auto sk = p->unsteps ? crc32_small_kernel<true> : crc32_small_kernel<false>;
+        auto sk = p->unsteps ? (dev_seeds ? crc32_small_kernel<true, true> : crc32_small_kernel<true, false>)
+                             : (dev_seeds ? crc32_small_kernel<false, true> : crc32_small_kernel<false, false>);
         hipLaunchKernelGGL(sk, dim3(p->grid), dim3(kThreads), 0, s,
                            reinterpret_cast<const uint8_t *>(dev_base), p->ustride, p->ua0, p->uvlen, p->uh,
                            p->W, p->desc, p->tiny, dev_seeds, dev_out, st->x8, st->xinv8, p->n, p->ntiny);
