@@ -8,8 +8,9 @@
 //
 // SHA-1 cannot be split inside a message (each 64-byte block depends on the
 // previous chaining value), so the unit of parallelism is one chunk per lane:
-// 1024 chunks = 16 waves.  This config is latency-bound on the dependent
-// round chain, not on HBM; DESIGN.md reports it as such.
+// 1024 chunks = 16 round waves.  This config is bound by the dependent round
+// chain, not by HBM; DESIGN.md reports it as such.  The message schedule runs
+// on a second wave (sha1_kernel).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -54,117 +55,198 @@ struct Sha1State {
     uint32_t h0, h1, h2, h3, h4;
 };
 
-__device__ __forceinline__ void sha1_block(Sha1State &st, uint32_t w[16])
+// Round function constants K_t (FIPS 180-4 §4.2.1).
+__device__ __forceinline__ constexpr uint32_t sha1_k(int t)
 {
-    uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
-#pragma unroll
-    for (int t = 0; t < 80; ++t) {
-        uint32_t wt;
-        if (t < 16) {
-            wt = w[t];
-        } else {
-            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
-            w[t & 15] = wt;
-        }
-        uint32_t f, k;
-        if (t < 20) {
-            f = ch3(b, c, d);                 // Ch
-            k = 0x5A827999u;
-        } else if (t < 40) {
-            f = xor3(b, c, d);                // Parity
-            k = 0x6ED9EBA1u;
-        } else if (t < 60) {
-            f = maj3(b, c, d);                // Maj
-            k = 0x8F1BBCDCu;
-        } else {
-            f = xor3(b, c, d);
-            k = 0xCA62C1D6u;
-        }
-        const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
-        e = d;
-        d = c;
-        c = rotl(b, 30);
-        b = a;
-        a = tmp;
-    }
-    st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+    return t < 20 ? 0x5A827999u : t < 40 ? 0x6ED9EBA1u : t < 60 ? 0x8F1BBCDCu : 0xCA62C1D6u;
 }
 
-__global__ void __launch_bounds__(64)
-sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-            const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests, uint32_t n)
+// Block j of lane's message as 16 big-endian words: content blocks, then the
+// 1 or 2 padding blocks (0x80, zeros, 64-bit bit length).
+__device__ __forceinline__ void message_block(const uint8_t *p, uint64_t len, uint64_t full, uint64_t j,
+                                              uint32_t w[16])
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) {
-        return;
-    }
-    const uint8_t *p = base + offs[i];
-    const uint64_t len = lens[i];
-    Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
-    uint32_t w[16];
-    const uint64_t full = len / 64;
-    if (((uintptr_t) p & 15u) == 0) {
-        // Aligned: block b+1 is loaded while block b is hashed (one wave per
-        // SIMD here, so nothing else would hide the HBM latency).
-        const uint4 *q = reinterpret_cast<const uint4 *>(p);
-        uint4 nx[4];
-        if (full > 0) {
+    if (j < full) {
+        const uint8_t *b = p + j * 64;
+        if (((uintptr_t) b & 15u) == 0) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(b);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                nx[v] = q[v];
+                const uint4 x = q[v];
+                w[4 * v + 0] = bswap32(x.x); w[4 * v + 1] = bswap32(x.y);
+                w[4 * v + 2] = bswap32(x.z); w[4 * v + 3] = bswap32(x.w);
             }
-        }
-        for (uint64_t blk = 0; blk < full; ++blk) {
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                w[4 * v + 0] = bswap32(nx[v].x); w[4 * v + 1] = bswap32(nx[v].y);
-                w[4 * v + 2] = bswap32(nx[v].z); w[4 * v + 3] = bswap32(nx[v].w);
-            }
-            const uint64_t pf = blk + 1 < full ? blk + 1 : blk;   // clamped: always in bounds
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                nx[v] = q[pf * 4 + v];
-            }
-            __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the rounds
-            sha1_block(st, w);
-        }
-    } else {
-        for (uint64_t blk = 0; blk < full; ++blk) {
-            const uint8_t *b = p + blk * 64;
+        } else {
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 w[t] = ((uint32_t) b[4 * t] << 24) | ((uint32_t) b[4 * t + 1] << 16) |
                        ((uint32_t) b[4 * t + 2] << 8) | (uint32_t) b[4 * t + 3];
             }
-            sha1_block(st, w);
         }
+        return;
     }
-    // Final block(s): remaining bytes, 0x80, zero pad, 64-bit big-endian bit length.
     const uint32_t rem = (uint32_t) (len - full * 64);
     const uint8_t *tail = p + full * 64;
-    const uint64_t bits = len * 8;
-    const int nfinal = rem < 56 ? 1 : 2;
-    for (int fb = 0; fb < nfinal; ++fb) {
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            uint32_t word = 0;
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t pos = (uint32_t) (fb * 64 + 4 * t + k);
-                uint32_t byte = 0;
-                if (pos < rem) {
-                    byte = tail[pos];
-                } else if (pos == rem) {
-                    byte = 0x80u;
-                }
-                word = (word << 8) | byte;
+    const uint32_t fb = (uint32_t) (j - full);
+    const uint32_t nfinal = rem < 56 ? 1u : 2u;
+    for (int t = 0; t < 16; ++t) {
+        uint32_t word = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pos = fb * 64 + 4 * t + k;
+            uint32_t byte = 0;
+            if (pos < rem) {
+                byte = tail[pos];
+            } else if (pos == rem) {
+                byte = 0x80u;
             }
-            w[t] = word;
+            word = (word << 8) | byte;
         }
-        if (fb == nfinal - 1) {
-            w[14] = (uint32_t) (bits >> 32);
-            w[15] = (uint32_t) bits;
+        w[t] = word;
+    }
+    if (fb == nfinal - 1) {
+        const uint64_t bits = len * 8;
+        w[14] = (uint32_t) (bits >> 32);
+        w[15] = (uint32_t) bits;
+    }
+}
+
+// One workgroup = two waves on two SIMDs for the same 64 chunks (one per
+// lane).  Wave 1 (schedule) loads each 64-byte block, expands the message
+// schedule and writes K_t + W_t for the 80 rounds to LDS; wave 0 (rounds)
+// runs only the dependent round chain, 5 instructions per round (rotate,
+// v_bitop3 round function, add3, add, rotate) instead of 7.5 with the schedule
+// inline.  The round chain of one chunk is the bound (one wave per SIMD, one
+// VALU instruction per 4 cycles), so halving its instruction stream is the
+// speed-up; two LDS slots let block j+1's schedule be built while block j's
+// rounds run, one barrier per block.
+constexpr int kShaRowsPerBlock = 20;   // 80 rounds as 20 rows of 4 (ds_read/write_b128)
+constexpr int kShaAhead = 4;           // blocks of message data in flight on the schedule wave
+
+__global__ void __launch_bounds__(128)
+sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+            const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests, uint32_t n)
+{
+    __shared__ uint4 kw[2][kShaRowsPerBlock][64];   // [slot][t / 4][lane] = K + W for t..t+3
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool sched = threadIdx.x >= 64;
+    const uint32_t i = blockIdx.x * 64 + lane;
+    const bool live = i < n;
+    const uint32_t ic = live ? i : n - 1;
+    const uint8_t *p = base + offs[ic];
+    const uint64_t len = lens[ic];
+    const uint64_t full = len / 64;
+    const uint64_t nblk = live ? full + ((len - full * 64) < 56 ? 1 : 2) : 0;
+    // The wave's block count: lanes with fewer blocks idle (masked) at the end.
+    uint64_t wmax = nblk;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        wmax = max(wmax, (uint64_t) __shfl_xor((unsigned long long) wmax, o));
+    }
+
+    if (sched) {
+        // Aligned content blocks come from a kShaAhead-deep register ring
+        // (block j + kShaAhead is requested when block j is consumed): the 64
+        // lanes read 64 chunks far apart, and one block of prefetch did not
+        // cover the HBM latency.
+        const bool aligned = ((uintptr_t) p & 15u) == 0;
+        const uint4 *q = reinterpret_cast<const uint4 *>(p);
+        uint4 nx[kShaAhead][4];
+#pragma unroll
+        for (int u = 0; u < kShaAhead; ++u) {
+            const uint64_t b = (uint64_t) u < full ? (uint64_t) u : (full ? full - 1 : 0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                nx[u][v] = (aligned && full > 0) ? q[b * 4 + v] : make_uint4(0, 0, 0, 0);
+            }
         }
-        sha1_block(st, w);
+        auto produce = [&](uint64_t j, uint4 (&r)[4]) {
+            if (j >= nblk) {
+                return;
+            }
+            uint32_t w[16];
+            if (aligned && j < full) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    w[4 * v + 0] = bswap32(r[v].x); w[4 * v + 1] = bswap32(r[v].y);
+                    w[4 * v + 2] = bswap32(r[v].z); w[4 * v + 3] = bswap32(r[v].w);
+                }
+                const uint64_t pf = j + kShaAhead < full ? j + kShaAhead : full - 1;   // clamped
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    r[v] = q[pf * 4 + v];
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the schedule
+            } else {
+                message_block(p, len, full, j, w);
+            }
+            uint4 *row = &kw[j & 1][0][lane];
+#pragma unroll
+            for (int r = 0; r < kShaRowsPerBlock; ++r) {
+                uint32_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = 4 * r + u;
+                    uint32_t wt;
+                    if (t < 16) {
+                        wt = w[t];
+                    } else {
+                        wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+                        w[t & 15] = wt;
+                    }
+                    v[u] = wt + sha1_k(t);
+                }
+                row[r * 64] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        };
+        // Block j's schedule is written before barrier j (wmax + 1 barriers,
+        // as on the round wave); unrolled so each ring slot is a fixed register set.
+        for (uint64_t jb = 0; jb <= wmax; jb += kShaAhead) {
+#pragma unroll
+            for (int u = 0; u < kShaAhead; ++u) {
+                if (jb + u <= wmax) {
+                    produce(jb + u, nx[u]);
+                    __syncthreads();
+                }
+            }
+        }
+        return;
+    }
+
+    Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    __syncthreads();
+    for (uint64_t j = 0; j < wmax; ++j) {
+        if (j < nblk) {
+            const uint4 *row = &kw[j & 1][0][lane];
+            // All 20 rows are requested up front (80 VGPRs; this wave is alone
+            // on its SIMD), so LDS latency is paid once per block, not per row.
+            uint4 rows[kShaRowsPerBlock];
+#pragma unroll
+            for (int r = 0; r < kShaRowsPerBlock; ++r) {
+                rows[r] = row[r * 64];
+            }
+            uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
+#pragma unroll
+            for (int r = 0; r < kShaRowsPerBlock; ++r) {
+                const uint4 q = rows[r];
+                const uint32_t kwv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = 4 * r + u;
+                    const uint32_t f = t < 20 ? ch3(b, c, d) : (t < 40 || t >= 60) ? xor3(b, c, d) : maj3(b, c, d);
+                    const uint32_t tmp = rotl(a, 5) + f + e + kwv[u];
+                    e = d;
+                    d = c;
+                    c = rotl(b, 30);
+                    b = a;
+                    a = tmp;
+                }
+            }
+            st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+        }
+        __syncthreads();
+    }
+    if (!live) {
+        return;
     }
     uint8_t *out = digests + (uint64_t) i * 20;
     const uint32_t h[5] = {st.h0, st.h1, st.h2, st.h3, st.h4};
@@ -199,7 +281,7 @@ extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, co
         e = hipMemcpyAsync(d + n, lens, n * sizeof(uint64_t), hipMemcpyHostToDevice, s);
     }
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(64), 0, s,
+        hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(128), 0, s,
                            reinterpret_cast<const uint8_t *>(dev_base), d, d + n, dev_digests,
                            (uint32_t) n);
         e = hipGetLastError();
