@@ -1716,7 +1716,24 @@ int cio_gpu_stream_sync(void *stream)
 
 namespace {
 
-constexpr size_t kStage = 64ull << 20;
+// Slot size: CIO_GPU_STAGE_MB (read once, when the pipeline is created),
+// default 64 MiB.  Smaller groups shorten the pipeline's fill and drain (the
+// first group's host copy and the last group's DMA are not overlapped).
+static size_t stage_bytes()
+{
+    static const size_t v = [] {
+        size_t mb = 64;
+        if (const char *r = getenv("CIO_GPU_STAGE_MB")) {
+            const long x = atol(r);
+            if (x >= 1 && x <= 1024) {
+                mb = (size_t) x;
+            }
+        }
+        return mb << 20;
+    }();
+    return v;
+}
+#define kStage (stage_bytes())
 constexpr int kSlots = 3;
 
 struct HostGroup {
