@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e", "perf"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    p.add_argument("--no-extra", action="store_true",
+                   help="cfg2 only: skip the 4 KiB (cfg4k) and 4 MiB (cfg4) lines reported in 'other_chunk_sizes'")
     p.add_argument("--ramp-ms", type=float, default=200.0,
                    help="untimed device ramp before the warmup steps (clocks/TLB; not counted as steps)")
     return p.parse_args()
@@ -463,6 +465,28 @@ def run_perf(args, rank, world, device, dist):
                              "crc_off_GBps": ref["crc_off"]["GBps"]}}
 
 
+def other_chunk_sizes(args, rank, world, device, dist):
+    """The north star's 4 KiB and 4 MiB chunk batches measured in the same run
+    (same process layout, same N), so every scaling run reports all three
+    chunk sizes: cfg4k (102 400 x 4 KiB per GPU, weak) and cfg4 (8192 x 4 MiB
+    per job, strong).  Same timing method as the headline line."""
+    import copy
+    import torch
+    out = {}
+    for cfg, steps, warm in (("cfg4k", 200, 50), ("cfg4", 20, 5)):
+        torch.cuda.empty_cache()
+        a = copy.copy(args)
+        a.config, a.steps, a.warmup, a.no_cpu = cfg, steps, warm, True
+        r = run_crc(a, rank, world, device, dist)
+        out[cfg] = {"value": r["value"], "unit": r["unit"], "scaling": r["scaling"], "steps": steps,
+                    "warmup": warm, "ms_per_step": r["ms_per_step"], "workload": r["config"]["workload"],
+                    "roofline": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "kernel",
+                                                                "kernel_ms_mean", "traffic")},
+                    "check": r.get("check", {})}
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     rank, world, device, dist = dist_setup(args)
@@ -474,6 +498,8 @@ def main():
         res = run_perf(args, rank, world, device, dist)
     else:
         res = run_crc(args, rank, world, device, dist)
+        if args.config == "cfg2" and not args.no_extra:
+            res["other_chunk_sizes"] = other_chunk_sizes(args, rank, world, device, dist)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:
