@@ -24,13 +24,13 @@ timeout -k 10 400 python bench.py --config $CFG > $OUT/bench_$TAG.json 2> $OUT/b
 stop_if_fatal $? bench
 cat $OUT/bench_$TAG.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- \
-    python3 bench.py --config $CFG --steps 300 --warmup 200 --no-cpu > $OUT/bench_prof_$TAG.json 2> $OUT/rocprof_$TAG.err
+    python3 bench.py --config $CFG --steps 300 --warmup 200 --no-cpu --no-extra > $OUT/bench_prof_$TAG.json 2> $OUT/rocprof_$TAG.err
 stop_if_fatal $? rocprof
 find $OUT/prof_$TAG -name "*stats*" | head
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$TAG -o run --output-format csv -- \
-    python3 bench.py --config $CFG --steps 20 --warmup 20 --no-cpu > /dev/null 2> $OUT/pmcf_$TAG.err
+    python3 bench.py --config $CFG --steps 20 --warmup 20 --no-cpu --no-extra > /dev/null 2> $OUT/pmcf_$TAG.err
 stop_if_fatal $? pmc_fetch
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$TAG -o run --output-format csv -- \
-    python3 bench.py --config $CFG --steps 20 --warmup 20 --no-cpu > /dev/null 2> $OUT/pmcw_$TAG.err
+    python3 bench.py --config $CFG --steps 20 --warmup 20 --no-cpu --no-extra > /dev/null 2> $OUT/pmcw_$TAG.err
 stop_if_fatal $? pmc_write
 python3 tools/pmc_traffic.py $OUT/pmcf_$TAG $OUT/pmcw_$TAG $CFG && cp profiles/pmc_$CFG.json $OUT/pmc_${CFG}_$TAG.json

@@ -3,8 +3,9 @@
 
     python tools/prof_window.py <run_kernel_trace.csv> <warmup> <steps> [kernel-substring]
 
-bench.py launches the CRC kernel `warmup` times, then `steps` timed launches
-back to back, then min(steps, 100) isolated diagnostic launches.  Prints the
+bench.py launches the CRC kernel during an untimed device ramp, then `warmup`
+times, then `steps` timed launches back to back, then min(steps, 100)
+isolated diagnostic launches (phases are located from the end).  Prints the
 mean / median / min duration of each phase (dispatches in start order) so the
 timed window can be compared with bench.py's `kernel_ms_mean`.
 """
@@ -23,8 +24,13 @@ def main():
     d = np.array([(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows])
     s = np.array([int(r["Start_Timestamp"]) / 1e3 for r in rows])
     out = {"kernel": name, "dispatches": len(d)}
-    phases = {"warmup": (0, warm), "timed": (warm, warm + steps),
-              "isolated": (warm + steps, warm + steps + min(steps, 100))}
+    # Counted from the end: bench.py's untimed device ramp (a variable number
+    # of launches) precedes the warmup steps.
+    iso = min(steps, 100)
+    end = len(d)
+    phases = {"ramp": (0, max(0, end - iso - steps - warm)),
+              "warmup": (max(0, end - iso - steps - warm), end - iso - steps),
+              "timed": (end - iso - steps, end - iso), "isolated": (end - iso, end)}
     for k, (a, b) in phases.items():
         x = d[a:b]
         if len(x):
