@@ -1040,18 +1040,31 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
 // 4 KiB wave-steps and the same coalesced non-temporal 16-byte loads, with the
 // CRC replaced by an XOR.  One 4-byte store per wave keeps the loads live.
 __global__ void __launch_bounds__(kThreads, 1)
-read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__restrict__ sink)
+read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__restrict__ sink, uint32_t B)
 {
     const uint32_t W = gridDim.x * (kThreads / kWave);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
     u32x4 acc = {0u, 0u, 0u, 0u};
-    for (uint64_t g = g0; g < g1; ++g) {
+    auto step = [&](uint64_t g) {
         const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * kGran);
 #pragma unroll
         for (int q = 0; q < kSub; ++q) {
             acc ^= __builtin_nontemporal_load(p + q * kWave);
+        }
+    };
+    if (B == 0) {
+        // the CRC kernel's split: one contiguous range per wave
+        const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
+        for (uint64_t g = g0; g < g1; ++g) {
+            step(g);
+        }
+    } else {
+        // diagnostic (CIO_GPU_RS_BLOCK=B): blocks of B steps dealt round-robin over the waves
+        for (uint64_t b = wave; b * B < S; b += W) {
+            for (uint64_t g = b * B; g < min(S, b * B + B); ++g) {
+                step(g);
+            }
         }
     }
     const uint32_t x = wave_xor(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]);
@@ -1647,9 +1660,13 @@ int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
     if (S == 0 || dev_base == nullptr) {
         return CIO_OK;
     }
+    uint32_t B = 0;
+    if (const char *r = getenv("CIO_GPU_RS_BLOCK")) {
+        B = (uint32_t) atoi(r);
+    }
     hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream),
-                       reinterpret_cast<const uint8_t *>(dev_base), S, sink);
+                       reinterpret_cast<const uint8_t *>(dev_base), S, sink, B);
     HIP_TRY(hipGetLastError(), "read_stream_kernel launch");
     return CIO_OK;
 }
