@@ -60,11 +60,20 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    # CIO_BENCH_REHEARSE=1: rehearse the N>1 path on a box with fewer GPUs
+    # than ranks (ranks share devices round-robin, gloo for the barrier and
+    # the max-over-ranks).  Never set by the driver's scaling runs.
+    rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     return rank, world, torch.device("cuda", local), dist
@@ -79,7 +88,8 @@ def max_over_ranks(x, dist, device):
     if dist is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    on_cpu = dist.get_backend() == "gloo"
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if on_cpu else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -271,6 +281,16 @@ def run_crc(args, rank, world, device, dist):
     elif args.config == "cfg4k" and rank == 0:
         from oracle import pyoracle as po
         check["cpu_oracle_match"] = bool(np.array_equal(po.crc_batch(bufs[0].cpu().numpy(), offs, lens), gpu0))
+    if world > 1:
+        # Every rank checks the first chunks of its own shard (chunk ids
+        # rank, rank + N, ...; contents regenerated on the host from the chunk
+        # id) against the CPU oracle; all ranks must agree.
+        from oracle import pyoracle as po
+        k = min(4, len(lens))
+        full_lens = np.zeros(int(ids[k - 1]) + 1, dtype=np.uint64)
+        full_lens[ids[:k].astype(np.int64)] = lens[:k]
+        ok = np.array_equal(po.crc_batch_chunks(seed, full_lens, idx=ids[:k].astype(np.int64)), gpu0[:k])
+        check["shard_sample_cpu_oracle_match_all_ranks"] = max_over_ranks(0.0 if ok else 1.0, dist, device) == 0.0
 
     res = {
         "metric": METRIC if args.config == "cfg2" else f"device-resident CRC32 GB/s ({args.config})",
