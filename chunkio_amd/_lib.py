@@ -20,6 +20,7 @@ EXPORTS = (
     "cio_crc32_shift", "cio_crc32_combine",
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_batch_dev", "cio_crc32_batch_host",
+    "cio_crc32_host_register", "cio_crc32_host_unregister",
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_gpu_read_stream",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
@@ -53,6 +54,8 @@ def _bind(lib):
         "cio_crc32_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, V, ctypes.c_size_t, V]),
         "cio_crc32_batch_host": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p,
                                                 ctypes.c_size_t]),
+        "cio_crc32_host_register": (ctypes.c_int, [V, ctypes.c_size_t]),
+        "cio_crc32_host_unregister": (ctypes.c_int, [V]),
         "cio_gpu_fill_synthetic": (ctypes.c_int, [V, c_u64_p, c_u64_p, c_u64_p, ctypes.c_size_t,
                                                   ctypes.c_uint64, V]),
         "cio_sha1_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, ctypes.c_size_t, V]),

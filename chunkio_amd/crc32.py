@@ -170,6 +170,18 @@ def crc32_batch_host(bufs, seeds=None):
     return out[:n]
 
 
+def host_register(arr):
+    """Pin a long-lived host buffer (numpy array / mmap view) in place so that
+    crc32_batch_host DMAs chunks inside it directly (no staging copy)."""
+    a = _as_bytes(arr)
+    _lib.check(_lib.lib().cio_crc32_host_register(a.ctypes.data, a.size), "cio_crc32_host_register")
+
+
+def host_unregister(arr):
+    a = _as_bytes(arr)
+    _lib.check(_lib.lib().cio_crc32_host_unregister(a.ctypes.data), "cio_crc32_host_unregister")
+
+
 def fill_synthetic(base, offs, lens, seed, ids=None, stream=None):
     """Fill chunks of a device buffer with the deterministic splitmix64 generator
     (chunk i uses generator index ids[i], default i)."""

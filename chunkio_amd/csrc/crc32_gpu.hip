@@ -2006,7 +2006,100 @@ hipError_t stage_plan(PipeSlot &s, const HostGroup &g, DeviceState *st, cio_crc3
     return hipSuccess;
 }
 
+// Host ranges pinned in place by cio_crc32_host_register (long-lived chunk
+// mappings).  A group whose every source lies inside one of them skips the
+// staging copy: the DMA engine reads the caller's pages directly.
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, size_t>> g_reg;   // (start, length)
+
+bool in_registered(const uint8_t *p, uint64_t len)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (const auto &r : g_reg) {
+        if (a >= r.first && a + len <= r.first + r.second) {
+            return true;
+        }
+    }
+    return false;
+}
+
+bool group_registered(const HostGroup &g)
+{
+    if (g_reg.empty()) {
+        return false;
+    }
+    for (size_t k = 0; k < g.src.size(); k++) {
+        if (g.lens[k] && !in_registered(g.src[k], g.lens[k])) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// Direct DMAs of a registered group into the slot's device buffer, one per
+// run of chunks that are adjacent both in host memory and in the group.
+hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
+{
+    size_t k = 0;
+    while (k < g.src.size()) {
+        if (g.lens[k] == 0) {
+            k++;
+            continue;
+        }
+        const uint8_t *src = g.src[k];
+        const uint64_t at = g.offs[k];
+        uint64_t len = g.lens[k];
+        size_t j = k + 1;
+        while (j < g.src.size() && g.src[j] == src + len && g.offs[j] == at + len) {
+            len += g.lens[j];
+            j++;
+        }
+        const hipError_t e = hipMemcpyAsync(dbuf + at, src, len, hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) {
+            return e;
+        }
+        k = j;
+    }
+    return hipSuccess;
+}
+
 }  // namespace
+
+extern "C" int cio_crc32_host_register(const void *p, size_t len)
+{
+    if (!p || len == 0) {
+        return fail("cio_crc32_host_register: empty range");
+    }
+    DeviceState *st;
+    if (device_state(&st) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto &r : g_reg) {
+        if (r.first == reinterpret_cast<uintptr_t>(p)) {
+            return fail("cio_crc32_host_register: already registered");
+        }
+    }
+    const hipError_t e = hipHostRegister(const_cast<void *>(p), len, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        return fail("cio_crc32_host_register", e);
+    }
+    g_reg.emplace_back(reinterpret_cast<uintptr_t>(p), len);
+    return CIO_OK;
+}
+
+extern "C" int cio_crc32_host_unregister(const void *p)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (size_t i = 0; i < g_reg.size(); i++) {
+        if (g_reg[i].first == reinterpret_cast<uintptr_t>(p)) {
+            const hipError_t e = hipHostUnregister(const_cast<void *>(p));
+            g_reg.erase(g_reg.begin() + (long) i);
+            return e == hipSuccess ? CIO_OK : fail("cio_crc32_host_unregister", e);
+        }
+    }
+    return fail("cio_crc32_host_unregister: not registered");
+}
 
 extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
                                     uint32_t *out_raw, size_t n)
@@ -2070,11 +2163,16 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
     if (e == hipSuccess) {
         e = hipStreamSynchronize(s0.stream);
     }
+    // Registered (pinned-in-place) sources: decided per group, under the
+    // registry lock for the whole call so a range cannot be unregistered
+    // while its DMAs are queued.
+    std::lock_guard<std::mutex> rlk(g_reg_mu);
     int rc = CIO_OK;
     hipEvent_t prev = nullptr;
     for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
         PipeSlot &s = hp->slot[gi % kSlots];
         const HostGroup &g = groups[gi];
+        const bool direct = group_registered(g);
         if (s.busy) {
             // The slot's previous group (gi - kSlots) must be fully done.
             if ((e = hipEventSynchronize(s.done)) != hipSuccess) break;
@@ -2089,9 +2187,13 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
             rc = fail(err);
             break;
         }
-        hp->pool->copy(s.pinned, g);
         if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
-        if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
+        if (direct) {
+            if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
+        } else {
+            hp->pool->copy(s.pinned, g);
+            if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
+        }
         if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
         if (plan_exec_impl(&view, s.dbuf, hp->state, hp->state, d_cid, s.stream) != CIO_OK) {
             rc = CIO_ERROR;

@@ -121,6 +121,18 @@ int  cio_crc32_batch_dev(const void *dev_base, const uint64_t *offs,
 int  cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
                           const uint32_t *seeds, uint32_t *out_raw, size_t n);
 
+/* Pin a long-lived host range in place (e.g. a chunk file's MAP_SHARED
+ * mapping, cio_file_unix.c:100) so that cio_crc32_batch_host DMAs the chunks
+ * inside it directly, skipping the copy into pinned staging.  A staging group
+ * takes the direct path only when every one of its chunks lies inside a
+ * registered range; others are staged as before, so results never depend on
+ * registration.  Registration pins pages (costly: do it once per mapping,
+ * not per batch).  CIO_ERROR when the driver cannot pin the range or it is
+ * already registered; cio_crc32_host_unregister(p) takes the start address
+ * given to register and must not race a batch call using the range. */
+int  cio_crc32_host_register(const void *p, size_t len);
+int  cio_crc32_host_unregister(const void *p);
+
 /* ---- synthetic data (benchmarks / tests) ------------------------------- */
 
 /* Fill dev_base + offs[i] .. + lens[i] with the deterministic generator

@@ -312,3 +312,48 @@ def test_host_pipeline_concurrent_callers(cuda):
         t.join()
     for k, bufs in enumerate(jobs):
         assert list(map(int, results[k])) == [po.crc_update(INIT, b) for b in bufs]
+
+
+@pytest.mark.gpu
+def test_host_registered_ranges_direct_dma(cuda, tmp_path):
+    """Chunks inside ranges pinned in place (cio_crc32_host_register) are
+    DMA'd directly; groups mixing registered and unregistered chunks are
+    staged.  Results are identical either way.  Covers an anonymous buffer and
+    a MAP_SHARED file mapping (chunkio's own buffers, cio_file_unix.c:100)."""
+    import mmap
+    rng = np.random.default_rng(13)
+    anon = mmap.mmap(-1, 96 << 20)
+    a = np.frombuffer(anon, dtype=np.uint8)
+    a[:] = rng.integers(0, 256, a.size, dtype=np.uint8)
+    path = tmp_path / "chunks.bin"
+    path.write_bytes(rng.integers(0, 256, 8 << 20, dtype=np.uint8).tobytes())
+    fd = open(path, "r+b")
+    fmap = mmap.mmap(fd.fileno(), 0, mmap.MAP_SHARED)
+    f = np.frombuffer(fmap, dtype=np.uint8)
+    loose = rng.integers(0, 256, 300000, dtype=np.uint8)
+    cuts = np.sort(rng.integers(0, a.size, 60))
+    bufs = [a[int(x):int(y)] for x, y in zip(cuts[:-1], cuts[1:])]       # adjacent runs
+    bufs += [a[5:409605], f[3:4000003], f[4000003:], a[:0], loose]
+    want = [po.crc_update(INIT, b) for b in bufs]
+    before = cio.crc32_batch_host(bufs)
+    cio.host_register(a)
+    try:
+        file_ok = True
+        try:
+            cio.host_register(f)
+        except cio.CioGpuError:
+            file_ok = False            # the driver may refuse file-backed pages
+        with pytest.raises(cio.CioGpuError):
+            cio.host_register(a)       # already registered
+        got = cio.crc32_batch_host(bufs)
+        only_a = cio.crc32_batch_host(bufs[:59])                         # all-registered groups
+        if file_ok:
+            cio.host_unregister(f)
+    finally:
+        cio.host_unregister(a)
+    with pytest.raises(cio.CioGpuError):
+        cio.host_unregister(a)
+    assert list(map(int, before)) == want
+    assert list(map(int, got)) == want
+    assert list(map(int, only_a)) == want[:59]
+    fd.close()
