@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident batched CRC-32 on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg4k|sha1|e2e|perf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg4k|sha1|e2e|perf|verify]
 
 One "step" = one pass of the hot path over one batch: crc_update(init, chunk)
 for every chunk of the batch (main kernel + per-chunk fold), inputs already
@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=200)
-    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e", "perf"])
+    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e", "perf", "verify"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--no-extra", action="store_true",
                    help="cfg2 only: skip the 4 KiB (cfg4k) and 4 MiB (cfg4) lines reported in 'other_chunk_sizes'")
@@ -507,6 +507,90 @@ def run_perf(args, rank, world, device, dist):
                              "crc_off_GBps": ref["crc_off"]["GBps"]}}
 
 
+def run_verify(args, rank, world, device, dist):
+    """batched verify-on-load of a stream directory.  1000
+    chunk files as `tools/cio -k -p` leaves them (2,068,480 B each: header,
+    5 x 400kb.txt, CRC 0x088740E7; one of them with a flipped content byte)
+    on the box's /tmp (page cache), verified by ONE cio_verify_paths call
+    (open + mmap + header/length checks + one batched GPU CRC pass + 8-byte
+    compare + munmap).  Beside it, the reference's per-file verify
+    (cio_file_format_check, src/cio_file.c:266-290: crc_update over
+    [22, 24 + meta + content) then compare) with the reference's own
+    crc_update (oracle/_ref), single thread, over the same mapped files."""
+    import shutil
+    from chunkio_amd import chunkfile as cf
+    d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8).tobytes()
+    files, bad = 1000, 500
+    reps = max(1, min(args.steps, 10))
+    root = tempfile.mkdtemp(prefix="cioa-verify-")
+    try:
+        paths = [os.path.join(root, f"perf-test-{i:04d}.txt") for i in range(files)]
+        c, _ = cf.ChunkFile.open(paths[0], deferred_crc=True)
+        for _ in range(5):
+            c.write(d400)
+        cf.sync_batch([c])
+        c.close()
+        for p in paths[1:]:
+            shutil.copyfile(paths[0], p)
+        with open(paths[bad], "r+b") as f:
+            f.seek(24 + 123456)
+            b = f.read(1)
+            f.seek(24 + 123456)
+            f.write(bytes([b[0] ^ 0x20]))
+        fsize = os.path.getsize(paths[0])
+        region = 2 + 5 * len(d400)              # [22, 24 + meta_len + content_len)
+        for _ in range(max(1, args.warmup)):
+            st, er, cr = cf.verify_paths(paths)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            st, er, cr = cf.verify_paths(paths)
+            times.append(time.perf_counter() - t0)
+        t = min(times)
+        ok_idx = [i for i in range(files) if i != bad]
+        check = {"good_files_ok": bool(np.all(st[ok_idx] == 0)),
+                 "good_crc_088740e7": bool(np.all((cr[ok_idx] ^ 0xFFFFFFFF) == 0x088740E7)),
+                 "flipped_file_bad_checksum": bool(st[bad] == -3 and er[bad] == -10)}
+        cpu = None
+        if rank == 0 and not args.no_cpu:
+            import mmap
+            from oracle import pyoracle as po
+            lib, kind = po.ref(), "reference"
+            fn = "crc_update"
+            if lib is None:
+                lib, kind, fn = po.oracle(), "port", "oracle_crc_update"
+            f_upd = getattr(lib, fn)
+            ncpu = 200
+            t0 = time.perf_counter()
+            nbad = 0
+            for p in paths[:ncpu]:
+                with open(p, "rb") as f:
+                    m = mmap.mmap(f.fileno(), 0, prot=mmap.PROT_READ)
+                    a = np.frombuffer(m, dtype=np.uint8)
+                    crc = int(f_upd(0xFFFFFFFF, a.ctypes.data + 22, region)) ^ 0xFFFFFFFF
+                    nbad += int(a[2:6].tobytes() != crc.to_bytes(4, "big"))
+                    del a
+                    m.close()
+            tc = time.perf_counter() - t0
+            cpu = {"value": round(ncpu * region / tc / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": kind,
+                   "sample": f"first {ncpu} of the same files: open + mmap + crc_update over the region + "
+                             "4-byte compare, one thread", "bad_found_in_sample": nbad}
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    res = {"metric": "batched verify-on-load GB/s (1000 chunk files from page cache, one cio_verify_paths call)",
+           "value": round(files * region / t / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": reps,
+           "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "tests/golden/400kb.txt x 5 per file (the reference's perf-test files)",
+           "config": {"workload": "verify-on-load of 1000 x 2,068,480-B chunk files (CRC region "
+                                  f"{region} B each), open/mmap/munmap included", "files": files,
+                      "file_bytes": fsize},
+           "check": check}
+    if cpu is not None:
+        res["cpu_baseline"] = cpu
+    return res
+
+
 def other_chunk_sizes(args, rank, world, device, dist):
     """The north star's 4 KiB and 4 MiB chunk batches measured in the same run
     (same process layout, same N), so every scaling run reports all three
@@ -538,6 +622,8 @@ def main():
         res = run_e2e(args, rank, world, device, dist)
     elif args.config == "perf":
         res = run_perf(args, rank, world, device, dist)
+    elif args.config == "verify":
+        res = run_verify(args, rank, world, device, dist)
     else:
         res = run_crc(args, rank, world, device, dist)
         if args.config == "cfg2" and not args.no_extra:
