@@ -357,3 +357,15 @@ def test_host_registered_ranges_direct_dma(cuda, tmp_path):
     assert list(map(int, got)) == want
     assert list(map(int, only_a)) == want[:59]
     fd.close()
+
+
+@pytest.mark.gpu
+def test_cfg2_tiled_400kb_full_size(cuda, data400):
+    """SURVEY §8(d) sanity batch at the full cfg2 size: 400kb.txt tiled
+    1024 times, every CRC finalizes to 0x777A8F30 (known answer, §8(c))."""
+    d = np.frombuffer(data400, np.uint8)
+    n = 1024
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(d.size)
+    lens = np.full(n, d.size, dtype=np.uint64)
+    got = gpu_crc(cuda, np.tile(d, n), offs, lens)
+    assert np.all((got ^ np.uint32(0xFFFFFFFF)) == np.uint32(0x777A8F30))
