@@ -161,6 +161,22 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
                      f"passes, crc_update(init, chunk) per chunk, deps/crc32/crc32.c "
                      f"{'compiled from the reference' if kind == 'reference' else 'oracle port'}, -O3",
            "bit_exact_vs_gpu": bool(np.array_equal(out, gpu_out))}
+    # the same batch over the box's CPU share (16 threads per
+    # GPU there), informational; `value`/`cores` above stay the 1-thread
+    # reference (chunkio itself is single-threaded).
+    nt = min(16, os.cpu_count() or 1)
+    f_mt = getattr(lib, prefix + "crc_batch_time_mt", None)
+    if f_mt is not None:
+        f_mt.restype = ctypes.c_double
+        f_mt.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                         ctypes.POINTER(ctypes.c_uint32)]
+        out_mt = np.zeros(n, dtype=np.uint32)
+        mreps = 4 * reps
+        secs_mt = f_mt(host_buf.ctypes.data, offs_c.ctypes.data_as(u64p), lens_c.ctypes.data_as(u64p), n,
+                       mreps, nt, out_mt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        res["multi_thread"] = {"value": round(float(lens_c.sum()) * mreps / secs_mt / 1e9, 3), "unit": "GB/s",
+                               "threads": nt, "bit_exact_vs_gpu": bool(np.array_equal(out_mt, gpu_out)),
+                               "sample": f"same batch x {mreps} passes, chunk i on thread i % {nt}"}
     # tools/cio -k -p restatement (BASELINE config 1), bounded sample of files.
     try:
         d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8)

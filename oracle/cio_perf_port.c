@@ -37,6 +37,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <arpa/inet.h>
+#include <pthread.h>
 
 #ifndef PORT_CRC_UPDATE
 #error "define PORT_CRC_UPDATE to the crc_update implementation to time"
@@ -189,6 +190,50 @@ double PORT_FN(crc_batch_time)(const unsigned char *base, const uint64_t *offs,
         for (size_t i = 0; i < n; i++) {
             out[i] = (uint32_t) PORT_CRC_UPDATE(0xffffffffu, base + offs[i], (size_t) lens[i]);
         }
+    }
+    return now_sec() - t1;
+}
+
+/* The same batch over `threads` host threads (chunk i -> thread i % threads),
+ * for SURVEY §8(d)'s "1 thread and nproc threads" CPU figure. */
+struct PORT_FN(mt_arg) {
+    const unsigned char *base;
+    const uint64_t *offs, *lens;
+    size_t n, t, threads;
+    int reps;
+    uint32_t *out;
+};
+
+static void *PORT_FN(mt_worker)(void *p)
+{
+    struct PORT_FN(mt_arg) *a = p;
+    for (int r = 0; r < a->reps; r++) {
+        for (size_t i = a->t; i < a->n; i += a->threads) {
+            a->out[i] = (uint32_t) PORT_CRC_UPDATE(0xffffffffu, a->base + a->offs[i], (size_t) a->lens[i]);
+        }
+    }
+    return NULL;
+}
+
+double PORT_FN(crc_batch_time_mt)(const unsigned char *base, const uint64_t *offs,
+                                  const uint64_t *lens, size_t n, int reps, int threads,
+                                  uint32_t *out)
+{
+    pthread_t tid[256];
+    struct PORT_FN(mt_arg) args[256];
+    if (threads < 1) {
+        threads = 1;
+    }
+    if (threads > 256) {
+        threads = 256;
+    }
+    double t1 = now_sec();
+    for (int t = 0; t < threads; t++) {
+        args[t] = (struct PORT_FN(mt_arg)) {base, offs, lens, n, (size_t) t, (size_t) threads, reps, out};
+        pthread_create(&tid[t], NULL, PORT_FN(mt_worker), &args[t]);
+    }
+    for (int t = 0; t < threads; t++) {
+        pthread_join(tid[t], NULL);
     }
     return now_sec() - t1;
 }

@@ -103,3 +103,23 @@ def test_cfg2_first_chunks(golden):
     g = golden["cfg2"]
     got = po.crc_batch_chunks(g["seed"], wl.cfg2_lens(), idx=range(8))
     assert list(got) == g["first32"][:8]
+
+
+def test_multithreaded_batch_timer_matches_single_thread():
+    """oracle's crc_batch_time_mt (the bench's nproc-thread CPU figure) gives
+    the same CRCs as the single-thread timer and the restatement."""
+    import ctypes
+    from chunkio_amd import workloads as wl
+    lens = np.asarray([0, 1, 7, 4096, 70001, 409600] * 5, dtype=np.uint64)
+    buf, offs = wl.host_batch(0x77, lens)
+    lib = po.oracle()
+    f = lib.oracle_crc_batch_time_mt
+    f.restype = ctypes.c_double
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    f.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_uint32)]
+    out = np.zeros(len(lens), np.uint32)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    f(buf.ctypes.data, offs.ctypes.data_as(u64p), lens.ctypes.data_as(u64p), len(lens), 2, 4,
+      out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    np.testing.assert_array_equal(out, po.crc_batch(buf, offs, lens))
