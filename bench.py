@@ -301,6 +301,17 @@ def run_crc(args, rank, world, device, dist):
         want = np.asarray([zlib.crc32(host0[int(o):int(o + n)]) ^ 0xFFFFFFFF for o, n in zip(offs, lens)],
                           dtype=np.uint32)
         check["zlib_match"] = bool(np.array_equal(want, gpu0))
+    if args.config in ("cfg3", "cfg4"):
+        # Full-size batches: 8 chunks spread over the batch (first, last and
+        # evenly between), device bytes copied back and CRC'd with zlib.
+        import zlib
+        pick = np.unique(np.linspace(0, len(lens) - 1, 8).astype(np.int64))
+        ok = True
+        for i in pick:
+            o, ln = int(offs[i]), int(lens[i])
+            ok &= (zlib.crc32(bufs[0][o:o + ln].cpu().numpy()) ^ 0xFFFFFFFF) == int(gpu0[i])
+        check["sample_zlib_match"] = bool(ok)
+        check["sample_chunks"] = [int(i) for i in pick]
     if world > 1:
         # Every rank checks the first chunks of its own shard (chunk ids
         # rank, rank + N, ...; contents regenerated on the host from the chunk
