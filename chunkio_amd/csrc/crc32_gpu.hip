@@ -355,7 +355,14 @@ __device__ __forceinline__ void load_step(StepRegs &r, const uint8_t *cbase, uin
     const uint64_t last = (vlen - 1) & ~15ull;
 #pragma unroll
     for (int q = 0; q < kSub; ++q) {
+#ifdef CIO_ABLATE_LOADS
+        // Diagnostic build only: compute without HBM (wrong CRCs).
+        const uint64_t a = min(b0 + (uint64_t) q * kRow, last) + (uint64_t) (uintptr_t) cbase;
+        r.q[q] = make_uint4((uint32_t) a, (uint32_t) (a >> 7) * 0x9E3779B9u, (uint32_t) a ^ 0x5bd1e995u,
+                            (uint32_t) (a >> 3) + 0x7f4a7c15u);
+#else
         r.q[q] = ldg16(cbase + min(b0 + (uint64_t) q * kRow, last));
+#endif
     }
 }
 
