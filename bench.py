@@ -94,6 +94,19 @@ def max_over_ranks(x, dist, device):
     return float(t.item())
 
 
+def gather_over_ranks(x, dist, device):
+    """[x of rank 0, x of rank 1, ...] (every rank gets the list)."""
+    if dist is None:
+        return [x]
+    import torch
+    on_cpu = dist.get_backend() == "gloo"
+    dev = "cpu" if on_cpu else device
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    out = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def geometry(cfg, rank, world):
     """(lens, ids, seed, workload description, scaling) of this rank's shard."""
     from chunkio_amd import workloads as wl
@@ -351,6 +364,11 @@ def run_crc(args, rank, world, device, dist):
                      "frac_of_read_stream": round(achieved / rs_gbs, 4)},
         "check": check,
     }
+    if world > 1:
+        # per-GPU rates beside the aggregate `value`.
+        res["per_gpu"] = {"achieved_GBps": [round(v, 1) for v in gather_over_ranks(achieved, dist, device)],
+                          "kernel_ms_mean": [round(v, 5) for v in gather_over_ranks(kernel_ms, dist, device)],
+                          "note": "rank order; each rank's algorithmic bytes / its kernel time"}
     if rank == 0 and world == 1 and not args.no_cpu and args.config == "cfg2":
         host = bufs[0].cpu().numpy()
         res["cpu_baseline"] = cpu_baseline(host, offs, lens, gpu0)
@@ -686,6 +704,8 @@ def other_chunk_sizes(args, rank, world, device, dist):
                     "roofline": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "kernel",
                                                                 "kernel_ms_mean", "traffic")},
                     "check": r.get("check", {})}
+        if "per_gpu" in r:
+            out[cfg]["per_gpu"] = r["per_gpu"]
     torch.cuda.empty_cache()
     return out
 

@@ -92,3 +92,34 @@ def test_bench_geometry_shards_cover_job():
             assert allids.tolist() == list(range(wl.CFG4_N))
         else:                  # weak scaling: 1024 chunks per GPU
             assert allids.tolist() == list(range(4 * wl.CFG2_N))
+
+
+def _gather_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        got = bench.gather_over_ranks(10.0 + rank, dist, "cpu")
+        mx = bench.max_over_ranks(float(rank), dist, "cpu")
+        if rank == 0:
+            q.put((got, mx))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_reductions_gloo_world2():
+    """bench.py's max-over-ranks and per-GPU gather on the gloo backend."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, mx = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == [10.0, 11.0]
+    assert mx == 1.0
