@@ -300,7 +300,7 @@ def run_crc(args, rank, world, device, dist):
         plan2 = cio.Crc32Plan(offs, lens)
         s2 = torch.cuda.Stream(device)
         pl = ((plan, stream), (plan2, s2))
-        for i in range(32):
+        for i in range(max(200, args.warmup)):
             p_, st_ = pl[i & 1]
             p_.exec(bufs[i % nrot], outs[i % nrot], stream=st_)
         torch.cuda.synchronize(device)
