@@ -14,10 +14,32 @@ CFLAGS   := -O3 -fPIC -Wall -Wextra -std=gnu11 $(INC)
 HIPFLAGS := -O3 -fPIC --offload-arch=$(ARCH) -std=c++17 -Wall $(INC) -munsafe-fp-atomics \
             -mllvm -amdgpu-atomic-optimizer-strategy=None -mllvm -amdgpu-kernarg-preload-count=8
 
-COBJS   := $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o
+COBJS   := $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o $(BLD)/cioa_chunk.o
 HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/sha1_gpu.o
 
-all: $(LIB) oracle
+CTEST   := tests/c/bin
+REF_INC := /root/reference/include/chunkio/cio_crc32.h
+CTESTS  := $(CTEST)/test_crc32_dropin $(CTEST)/test_chunk_api $(if $(wildcard $(REF_INC)),$(CTEST)/test_crc32_dropin_ref)
+CLINK   := -Lchunkio_amd/lib -lchunkio_amd -Wl,-rpath,'$$ORIGIN/../../../chunkio_amd/lib'
+
+all: $(LIB) oracle ctests
+
+# C callers of the public headers (tests/test_c_api.py runs them).  The _ref
+# variant compiles the reference's own include/chunkio/cio_crc32.h, unmodified,
+# against include/crc32/crc32.h (only where /root/reference exists).
+ctests: $(CTESTS)
+
+$(CTEST)/test_crc32_dropin: tests/c/test_crc32_dropin.c $(LIB) include/crc32/crc32.h
+	@mkdir -p $(CTEST)
+	$(CC) -O2 -Wall -Wextra -std=gnu11 -Iinclude -o $@ $< $(CLINK)
+
+$(CTEST)/test_crc32_dropin_ref: tests/c/test_crc32_dropin.c $(LIB) include/crc32/crc32.h
+	@mkdir -p $(CTEST)
+	$(CC) -O2 -Wall -Wextra -std=gnu11 -DCIOA_REF_BOUNDARY -Iinclude -I/root/reference/include -o $@ $< $(CLINK)
+
+$(CTEST)/test_chunk_api: tests/c/test_chunk_api.c $(LIB) $(wildcard include/*/*.h)
+	@mkdir -p $(CTEST)
+	$(CC) -O2 -Wall -Wextra -std=gnu11 -Iinclude -o $@ $< $(CLINK)
 
 $(BLD)/%.o: $(SRC)/%.c $(wildcard $(SRC)/*.h) $(wildcard include/*/*.h)
 	@mkdir -p $(BLD)
@@ -39,7 +61,7 @@ asm: $(SRC)/crc32_gpu.hip
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(BLD)/asm/crc32_gpu.s $<
 
 clean:
-	rm -rf $(BLD) $(LIB)
+	rm -rf $(BLD) $(LIB) $(CTEST)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all oracle asm clean ctests

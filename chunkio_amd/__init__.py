@@ -5,13 +5,14 @@ Layers:
   include/crc32/crc32.h, include/chunkio_amd/*.h   C ABI (the drop-in boundary)
   chunkio_amd/csrc/*.hip, *.c                      HIP kernels for gfx950 + host C
   chunkio_amd/crc32.py                             Python mirror of the CRC API
-  chunkio_amd/chunkfile.py                         chunk-file layer (write/sync/verify)
+  chunkio_amd/chunkfile.py                         binding of the C chunk layer
+                                                   (cioa_chunk.h: write/sync/verify/tx/scan)
 """
 from ._lib import LIB_PATH, CioGpuError, lib  # noqa: F401
 from .crc32 import (  # noqa: F401
     CRC_INIT, Crc32Plan, crc32, crc32_batch_dev, crc32_batch_host, crc32_combine,
-    crc32_shift, crc_finalize, crc_init, crc_update, fill_synthetic, host_register,
+    crc32_shift, crc_finalize, crc_init, crc_update, device_count, fill_synthetic, host_register,
     host_unregister, sha1_batch_dev,
 )
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"

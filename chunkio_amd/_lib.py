@@ -20,14 +20,27 @@ EXPORTS = (
     "cio_crc32_shift", "cio_crc32_combine",
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_batch_dev", "cio_crc32_batch_host",
+    "cio_crc32_batch_host_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device",
     "cio_crc32_host_register", "cio_crc32_host_unregister",
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_gpu_read_stream",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
     # include/chunkio_amd/cio_verify.h
-    "cio_file_verify_batch", "cio_verify_paths",
+    "cio_file_verify_batch", "cio_file_verify_batch_multi", "cio_verify_paths", "cio_verify_paths_multi",
     # include/chunkio_amd/cio_sync.h
-    "cio_file_sync_batch",
+    "cio_file_sync_batch", "cio_file_sync_batch_multi",
+    # include/chunkio_amd/cioa_chunk.h
+    "cioa_create", "cioa_destroy", "cioa_set_max_chunks_up", "cioa_set_realloc_size_hint",
+    "cioa_enable_file_trimming", "cioa_disable_file_trimming", "cioa_get_flags", "cioa_set_devices",
+    "cioa_last_chunk_error", "cioa_total_chunks", "cioa_total_chunks_up",
+    "cioa_stream_create", "cioa_stream_get", "cioa_stream_size_chunks_up", "cioa_stream_chunks", "cioa_scan_stream",
+    "cioa_chunk_open", "cioa_chunk_close", "cioa_chunk_delete", "cioa_chunk_write", "cioa_chunk_write_at",
+    "cioa_chunk_sync", "cioa_chunk_sync_batch", "cioa_chunk_get_content", "cioa_chunk_get_content_copy",
+    "cioa_chunk_get_content_size", "cioa_chunk_get_real_size", "cioa_chunk_hash", "cioa_chunk_lock",
+    "cioa_chunk_unlock", "cioa_chunk_is_locked", "cioa_chunk_tx_begin", "cioa_chunk_tx_commit",
+    "cioa_chunk_tx_rollback", "cioa_chunk_is_up", "cioa_chunk_up", "cioa_chunk_up_force", "cioa_chunk_down",
+    "cioa_chunk_name", "cioa_chunk_map", "cioa_error_get", "cioa_chunk_crc_cur", "cioa_chunk_set_crc_cur",
+    "cioa_meta_write", "cioa_meta_read", "cioa_meta_cmp", "cioa_meta_size", "cioa_bench_perf_write",
 )
 
 _lib = None
@@ -54,6 +67,11 @@ def _bind(lib):
         "cio_crc32_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, V, ctypes.c_size_t, V]),
         "cio_crc32_batch_host": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p,
                                                 ctypes.c_size_t]),
+        "cio_crc32_batch_host_multi": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p,
+                                                      ctypes.c_size_t, P(ctypes.c_int), ctypes.c_int]),
+        "cio_gpu_device_count": (ctypes.c_int, []),
+        "cio_gpu_set_device": (ctypes.c_int, [ctypes.c_int]),
+        "cio_gpu_get_device": (ctypes.c_int, []),
         "cio_crc32_host_register": (ctypes.c_int, [V, ctypes.c_size_t]),
         "cio_crc32_host_unregister": (ctypes.c_int, [V]),
         "cio_gpu_fill_synthetic": (ctypes.c_int, [V, c_u64_p, c_u64_p, c_u64_p, ctypes.c_size_t,

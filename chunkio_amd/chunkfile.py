@@ -1,63 +1,49 @@
-"""Chunk-file layer: the reference's on-disk format and CRC lifecycle, host side.
+"""Python binding of the C chunk layer (include/chunkio_amd/cioa_chunk.h).
 
-Mirrors fluent/chunkio's filesystem backend for one chunk (names follow the
-reference's functions; file:line citations into /root/reference):
+The chunk layer itself is C (chunkio_amd/csrc/cioa_chunk.c): chunkio's
+filesystem backend with the reference's on-disk format and CRC lifecycle,
+its verifies and deferred CRCs on the batched GPU path.  Names follow the
+reference (file:line citations into /root/reference):
 
-  ChunkFile.open(path, flags)     cio_file_open + mmap_file + cio_file_format_check
-                                  (src/cio_file.c:636-782, 345-493, 187-294)
-  ChunkFile.write(data)           cio_file_write (src/cio_file.c:994-1073):
-                                  grow in realloc_size steps (8 pages,
-                                  include/chunkio/chunkio.h:59-66), update_checksum
-                                  (:97-113, raw 8-byte state at map+2), copy, BE length
-  ChunkFile.write_at(data, off)   cio_chunk_write_at (src/cio_chunk.c:184-209): truncate
-                                  + crc_reset -> full recompute on the next write
-  ChunkFile.write_metadata(meta)  cio_file_write_metadata + adjust_layout (:1075-1145, 130-146)
-  ChunkFile.sync()                cio_file_sync (:1147-1250): finalize_checksum (:116-124)
-  ChunkFile.hash()                cio_file_hash (:1304-1307): the 4 bytes at map+2
-  ChunkFile.down()/up()           munmap_file / _cio_file_up (re-verify on map)
+  Context(root, flags)            cio_create (src/chunkio.c:84-207)
+  Context.stream(name)            cio_stream_create (src/cio_stream.c:113-178)
+  Context.scan(stream, ext)       cio_scan_stream_files (src/cio_scan.c:39-125), one
+                                  GPU verify batch, CIO_DELETE_IRRECOVERABLE
+  Stream.open(name, flags)        cio_chunk_open (src/cio_chunk.c:30-109)
+  Chunk.write / write_at          cio_chunk_write / _write_at (src/cio_chunk.c:184-227)
+  Chunk.meta_write / meta_len     cio_meta_write / _size (src/cio_meta.c:46-88)
+  Chunk.sync / sync_batch(chunks) cio_chunk_sync (src/cio_file.c:1147-1250); batched
+  Chunk.up / up_force / down      src/cio_chunk.c:556-605
+  Chunk.tx_begin/commit/rollback  src/cio_chunk.c:423-502
+  Chunk.hash()                    cio_chunk_hash: the 4 bytes at map+2
 
-Every CRC of a whole region (verify on open/up, metadata recompute) goes
-through the batched GPU path (cio_file_verify_batch / cio_crc32_batch_host);
-the incremental per-write update uses crc_update on the caller's buffer, as
-the reference does at src/cio_file.c:110.
+ChunkFile.open(path, ...) is the one-chunk convenience form used by the
+tests and benches: a private context rooted at dirname(dirname(path)) with
+the stream dirname(path).
 
-verify_paths(paths) is the batched verify-on-load of a stream directory
-(cio_scan_stream_files, src/cio_scan.c:39-125) in one GPU pass.
-
-ChunkFile(..., deferred_crc=True) takes the CRC off the append path: write()
-only copies (no crc_update, no raw state at map+2) and sync_batch(files)
-brings every dirty chunk's CRC up to date in one GPU pass seeded with its
-crc_cur (cio_file_sync_batch, include/chunkio_amd/cio_sync.h).  After the sync
-the file bytes are identical to the reference's write/sync sequence; between
-a write and the sync, map+2 (cio_file_hash) still holds the previous header.
+verify_paths(paths) is the batched verify-on-load of a list of chunk files
+(cio_verify_paths_multi).
 """
 import ctypes
-import mmap
 import os
 import struct
 
 import numpy as np
 
 from . import _lib
-from .crc32 import crc_update
 
 CIO_OK, CIO_ERROR, CIO_RETRY, CIO_CORRUPTED = 0, -1, -2, -3
-CIO_OPEN, CIO_OPEN_RD, CIO_CHECKSUM = 1, 2, 4
+CIO_OPEN, CIO_OPEN_RD, CIO_CHECKSUM, CIO_FULL_SYNC = 1, 2, 4, 8
+CIO_DELETE_IRRECOVERABLE, CIO_TRIM_FILES = 16, 32
+CIOA_DEFERRED_CRC = 128
 CIO_ERR_BAD_CHECKSUM, CIO_ERR_BAD_LAYOUT, CIO_ERR_PERMISSION, CIO_ERR_BAD_FILE_SIZE = -10, -11, -12, -13
+CIOA_VERIFY_DELETE_IRRECOVERABLE = 16
 CIOA_VERIFY_WRITEBACK = 64
-CIOA_SYNC_FINALIZE, CIOA_SYNC_MSYNC = 1, 2
+CIOA_SYNC_FINALIZE, CIOA_SYNC_MSYNC, CIOA_SYNC_FULL = 1, 2, 8
 
 HDR_MIN = 24
 CONTENT_OFFSET = 22
-CONTENT_LEN_OFFSET = 10
-# cio_file_init_bytes (src/cio_file.c:45-60): C1 00, CRC32("\0\0") LE, zeros
-INIT_BYTES = bytes([0xC1, 0x00, 0xFF, 0x12, 0xD9, 0x41]) + bytes(18)
 CRC_INIT = 0xFFFFFFFF
-PAGE = mmap.PAGESIZE
-
-
-def _round_up(n, s):
-    return ((n + s - 1) // s) * s
 
 
 class VerifyItem(ctypes.Structure):
@@ -68,25 +54,79 @@ class VerifyItem(ctypes.Structure):
 
 class SyncItem(ctypes.Structure):
     _fields_ = [("map", ctypes.c_void_p), ("fs_size", ctypes.c_size_t), ("crc_end", ctypes.c_uint64),
-                ("crc_cur", ctypes.c_uint32), ("status", ctypes.c_int)]
+                ("crc_cur", ctypes.c_uint32), ("status", ctypes.c_int), ("data_end", ctypes.c_uint64)]
 
 
 def _bind():
     lib = _lib.lib()
-    if not hasattr(lib, "_verify_bound"):
-        lib.cio_file_verify_batch.restype = ctypes.c_int
-        lib.cio_file_verify_batch.argtypes = [ctypes.POINTER(VerifyItem), ctypes.c_size_t, ctypes.c_int]
-        lib.cio_verify_paths.restype = ctypes.c_int
-        lib.cio_verify_paths.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_int,
-                                         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
-                                         ctypes.POINTER(ctypes.c_uint32)]
-        lib.cio_file_sync_batch.restype = ctypes.c_int
-        lib.cio_file_sync_batch.argtypes = [ctypes.POINTER(SyncItem), ctypes.c_size_t, ctypes.c_int]
-        lib._verify_bound = True
+    if getattr(lib, "_chunk_bound", False):
+        return lib
+    V, I, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    IP, U32 = ctypes.POINTER(ctypes.c_int), ctypes.c_uint32
+    sig = {
+        "cio_file_verify_batch": (I, [ctypes.POINTER(VerifyItem), S, I]),
+        "cio_file_verify_batch_multi": (I, [ctypes.POINTER(VerifyItem), S, I, IP, I]),
+        "cio_verify_paths": (I, [ctypes.POINTER(ctypes.c_char_p), S, I, IP, IP, ctypes.POINTER(U32)]),
+        "cio_verify_paths_multi": (I, [ctypes.POINTER(ctypes.c_char_p), S, I, IP, I, IP, IP,
+                                       ctypes.POINTER(U32)]),
+        "cio_file_sync_batch": (I, [ctypes.POINTER(SyncItem), S, I]),
+        "cio_file_sync_batch_multi": (I, [ctypes.POINTER(SyncItem), S, I, IP, I]),
+        "cioa_create": (V, [ctypes.c_char_p, I]),
+        "cioa_destroy": (None, [V]),
+        "cioa_set_max_chunks_up": (I, [V, I]),
+        "cioa_set_realloc_size_hint": (I, [V, S]),
+        "cioa_set_devices": (I, [V, IP, I]),
+        "cioa_last_chunk_error": (I, [V]),
+        "cioa_total_chunks_up": (S, [V]),
+        "cioa_stream_create": (V, [V, ctypes.c_char_p]),
+        "cioa_stream_get": (V, [V, ctypes.c_char_p]),
+        "cioa_stream_chunks": (S, [V, ctypes.POINTER(V), S]),
+        "cioa_stream_size_chunks_up": (S, [V]),
+        "cioa_scan_stream": (V, [V, ctypes.c_char_p, ctypes.c_char_p]),
+        "cioa_chunk_open": (V, [V, V, ctypes.c_char_p, I, S, IP]),
+        "cioa_chunk_close": (None, [V, I]),
+        "cioa_chunk_write": (I, [V, V, S]),
+        "cioa_chunk_write_at": (I, [V, ctypes.c_long, V, S]),
+        "cioa_chunk_sync": (I, [V]),
+        "cioa_chunk_sync_batch": (I, [ctypes.POINTER(V), S]),
+        "cioa_chunk_get_content_size": (ctypes.c_ssize_t, [V]),
+        "cioa_chunk_get_real_size": (ctypes.c_ssize_t, [V]),
+        "cioa_chunk_hash": (V, [V]),
+        "cioa_chunk_map": (V, [V, ctypes.POINTER(S)]),
+        "cioa_chunk_name": (ctypes.c_char_p, [V]),
+        "cioa_chunk_lock": (I, [V]),
+        "cioa_chunk_unlock": (I, [V]),
+        "cioa_chunk_tx_begin": (I, [V]),
+        "cioa_chunk_tx_commit": (I, [V]),
+        "cioa_chunk_tx_rollback": (I, [V]),
+        "cioa_chunk_is_up": (I, [V]),
+        "cioa_chunk_up": (I, [V]),
+        "cioa_chunk_up_force": (I, [V]),
+        "cioa_chunk_down": (I, [V]),
+        "cioa_error_get": (I, [V]),
+        "cioa_chunk_crc_cur": (U32, [V]),
+        "cioa_chunk_set_crc_cur": (None, [V, U32]),
+        "cioa_meta_write": (I, [V, ctypes.c_char_p, S]),
+        "cioa_meta_size": (I, [V]),
+        "cioa_bench_perf_write": (I, [ctypes.c_char_p, V, S, I, I, I, I, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    lib._chunk_bound = True
     return lib
 
 
-def verify_paths(paths, flags=CIO_CHECKSUM):
+def _devs(devices):
+    if not devices:
+        return None, 0
+    arr = (ctypes.c_int * len(devices))(*devices)
+    return arr, len(devices)
+
+
+def verify_paths(paths, flags=CIO_CHECKSUM, devices=None):
     """Batched verify-on-load: (status, error, crc_raw) numpy arrays per path."""
     lib = _bind()
     n = len(paths)
@@ -94,253 +134,274 @@ def verify_paths(paths, flags=CIO_CHECKSUM):
     st = np.zeros(max(n, 1), np.int32)
     er = np.zeros(max(n, 1), np.int32)
     cr = np.zeros(max(n, 1), np.uint32)
-    rc = lib.cio_verify_paths(arr, n, flags, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-                              er.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-                              cr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
-    _lib.check(rc, "cio_verify_paths")
+    dv, nd = _devs(devices)
+    rc = lib.cio_verify_paths_multi(arr, n, flags, dv, nd, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                    er.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                    cr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    _lib.check(rc, "cio_verify_paths_multi")
     return st[:n], er[:n], cr[:n]
 
 
-def sync_batch(files):
-    """Sync many chunk files at once: the deferred-CRC ones through ONE GPU
-    batch (cio_file_sync_batch, finalize + msync), the others one by one."""
-    dirty = [f for f in files if f.map is not None and not f.synced and (f.flags & CIO_OPEN)]
-    batch = [f for f in dirty if f.deferred_crc and (f.flags & CIO_CHECKSUM)]
-    for f in dirty:
-        if f not in batch:
-            f.sync()
-    if not batch:
-        return CIO_OK
-    items = (SyncItem * len(batch))()
-    views = []
-    for it, f in zip(items, batch):
-        v = (ctypes.c_char * f.alloc_size).from_buffer(f.map)
-        views.append(v)
-        it.map = ctypes.addressof(v)
-        it.fs_size = f.alloc_size
-        it.crc_end = f.crc_end
-        it.crc_cur = f.crc_cur
-    rc = _bind().cio_file_sync_batch(items, len(batch), CIOA_SYNC_FINALIZE | CIOA_SYNC_MSYNC)
-    del views
-    _lib.check(rc, "cio_file_sync_batch")
-    for it, f in zip(items, batch):
-        if it.status != CIO_OK:
-            f.error = CIO_ERR_BAD_LAYOUT
-            continue
-        f.crc_cur = int(it.crc_cur)
-        f.crc_end = int(it.crc_end)
-        f.synced = True
-        f.fs_size = os.fstat(f.fd).st_size
-    return CIO_OK
+class Context:
+    """cio_ctx: a root directory of streams of chunk files."""
 
+    def __init__(self, root, flags=CIO_CHECKSUM, devices=None, max_chunks_up=None):
+        self._lib = _bind()
+        self.root = root
+        self._h = self._lib.cioa_create(os.fsencode(root), flags)
+        if not self._h:
+            raise OSError(f"cioa_create({root!r}) failed")
+        if devices:
+            dv, nd = _devs(devices)
+            self._lib.cioa_set_devices(self._h, dv, nd)
+        if max_chunks_up is not None:
+            self._lib.cioa_set_max_chunks_up(self._h, int(max_chunks_up))
+        self._chunks = []
 
-class ChunkFile:
-    """One filesystem chunk with the reference's layout and CRC semantics."""
+    def stream(self, name):
+        h = self._lib.cioa_stream_get(self._h, name.encode()) or self._lib.cioa_stream_create(self._h, name.encode())
+        if not h:
+            raise OSError(f"cannot create stream {name!r}")
+        return Stream(self, h, name)
 
-    def __init__(self, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None, deferred_crc=False):
-        self.path = path
-        self.flags = flags
-        self.deferred_crc = deferred_crc
-        self.crc_end = CONTENT_OFFSET     # file offset up to which crc_cur is current
-        self.realloc_size = realloc_size or PAGE * 8
-        self.fd = -1
-        self.map = None
-        self.alloc_size = 0
-        self.fs_size = 0
-        self.data_size = 0
-        self.crc_cur = CRC_INIT
-        self.crc_reset = False
-        self.taint = False
-        self.synced = True
-        self.error = 0
+    def scan(self, stream, ext=None):
+        """Load a stream directory (one batched GPU verify): (Stream, [Chunk])."""
+        h = self._lib.cioa_scan_stream(self._h, stream.encode(), ext.encode() if ext else None)
+        if not h:
+            raise OSError(f"cannot scan stream {stream!r}")
+        st = Stream(self, h, stream)
+        return st, st.chunks()
 
-    # -- open / map -------------------------------------------------------
-    @classmethod
-    def open(cls, path, flags=CIO_OPEN | CIO_CHECKSUM, realloc_size=None, deferred_crc=False):
-        cf = cls(path, flags, realloc_size, deferred_crc)
-        rc = cf.up()
-        if rc != CIO_OK:
-            cf._close_fd()
-        return cf, rc
+    @property
+    def last_chunk_error(self):
+        return int(self._lib.cioa_last_chunk_error(self._h))
 
-    def up(self):
-        """Open + map + format check (src/cio_file.c:345-493, 187-294)."""
-        if self.map is not None:
-            return CIO_OK
-        rw = bool(self.flags & CIO_OPEN)
-        self.fd = os.open(self.path, (os.O_RDWR | os.O_CREAT) if rw else os.O_RDONLY, 0o600)
-        fs_size = os.fstat(self.fd).st_size
-        self.taint = False
-        if fs_size == 0:
-            if not rw:
-                self.error = CIO_ERR_PERMISSION
-                return CIO_CORRUPTED
-            size = _round_up(HDR_MIN, PAGE)
-            os.posix_fallocate(self.fd, 0, size)
-            self.alloc_size = size
-            self.map = mmap.mmap(self.fd, size)
-            self.map[:HDR_MIN] = INIT_BYTES
-            if not (self.flags & CIO_CHECKSUM):
-                self.map[2:6] = bytes(4)
-            self._set_content_len(0)
-            self.data_size = 0
-            self.fs_size = 0
-            self.synced = False
-            if self.flags & CIO_CHECKSUM:
-                self.crc_cur = crc_update(CRC_INIT, self.map[CONTENT_OFFSET:CONTENT_OFFSET + 2])
-                self.crc_end = HDR_MIN
-            return CIO_OK
-        prot = mmap.PROT_READ | (mmap.PROT_WRITE if rw else 0)
-        self.map = mmap.mmap(self.fd, fs_size, prot=prot)
-        self.alloc_size = fs_size
-        self.fs_size = fs_size
-        self.synced = True
-        # header checks + (batched, GPU) CRC verify of this one chunk
-        item = (VerifyItem * 1)()
-        if rw:
-            view = (ctypes.c_char * fs_size).from_buffer(self.map)
-            addr = ctypes.addressof(view)
-        else:
-            view = np.frombuffer(self.map, dtype=np.uint8)
-            addr = view.ctypes.data
-        item[0].map = addr
-        item[0].fs_size = fs_size
-        item[0].taint = 0
-        vflags = (self.flags & CIO_CHECKSUM) | (CIOA_VERIFY_WRITEBACK if rw else 0)
-        _lib.check(_bind().cio_file_verify_batch(item, 1, vflags), "cio_file_verify_batch")
-        del view
-        self.error = item[0].error
-        if item[0].status != CIO_OK:
-            # cio_file_format_check failure: map released, fd closed (tests/fs.c:719-722)
-            self.map.close()
-            self.map = None
-            self._close_fd()
-            return CIO_CORRUPTED
-        self.data_size = int(item[0].content_len)
-        if self.flags & CIO_CHECKSUM:
-            self.crc_cur = int(item[0].crc_raw)
-            self.crc_end = HDR_MIN + self.meta_len() + self.data_size
-        return CIO_OK
-
-    def down(self):
-        if self.map is None:
-            return CIO_ERROR
-        if not self.synced:
-            self.sync()
-        self.map.close()
-        self.map = None
-        self._close_fd()
-        return CIO_OK
+    @property
+    def total_chunks_up(self):
+        return int(self._lib.cioa_total_chunks_up(self._h))
 
     def close(self):
-        if self.map is not None:
-            self.down()
-        self._close_fd()
+        if self._h:
+            for c in self._chunks:
+                c._h = None
+            self._lib.cioa_destroy(self._h)
+            self._h = None
 
-    def _close_fd(self):
-        if self.fd >= 0:
-            os.close(self.fd)
-            self.fd = -1
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
-    # -- layout helpers (include/chunkio/cio_file_st.h) -----------------------
-    def meta_len(self):
-        return (self.map[CONTENT_OFFSET] << 8) | self.map[CONTENT_OFFSET + 1]
+    def __enter__(self):
+        return self
 
-    def _set_content_len(self, n):
-        self.map[CONTENT_LEN_OFFSET:CONTENT_LEN_OFFSET + 4] = struct.pack(">I", n)
+    def __exit__(self, *exc):
+        self.close()
 
-    def content(self):
-        off = HDR_MIN + self.meta_len()
-        return bytes(self.map[off:off + self.data_size])
 
-    def hash(self):
-        return bytes(self.map[2:6])
+class Stream:
+    def __init__(self, ctx, h, name):
+        self.ctx, self._h, self.name = ctx, h, name
 
-    def _region_crc(self):
-        """crc_update(init, map+22, 2 + meta + data) -- cio_file_calculate_checksum."""
-        from .crc32 import crc32_batch_host
-        n = 2 + self.meta_len() + self.data_size
-        view = np.frombuffer(self.map, dtype=np.uint8)[CONTENT_OFFSET:CONTENT_OFFSET + n]
-        return int(crc32_batch_host([view])[0])
+    def open(self, name, flags=CIO_OPEN, size=0):
+        """(Chunk or None, err)."""
+        err = ctypes.c_int(0)
+        h = self.ctx._lib.cioa_chunk_open(self.ctx._h, self._h, name.encode(), flags, size, ctypes.byref(err))
+        if not h:
+            return None, int(err.value)
+        c = Chunk(self.ctx, h)
+        self.ctx._chunks.append(c)
+        return c, CIO_OK
 
-    # -- writes ---------------------------------------------------------------
-    def _resize(self, new_size):
-        os.posix_fallocate(self.fd, 0, new_size)
-        self.map.resize(new_size)
-        self.alloc_size = new_size
-        self.fs_size = new_size
+    def chunks(self):
+        lib = self.ctx._lib
+        n = int(lib.cioa_stream_chunks(self._h, None, 0))
+        arr = (ctypes.c_void_p * max(n, 1))()
+        lib.cioa_stream_chunks(self._h, arr, n)
+        known = {c._h: c for c in self.ctx._chunks if c._h}
+        out = []
+        for i in range(n):
+            c = known.get(arr[i])
+            if c is None:
+                c = Chunk(self.ctx, arr[i])
+                self.ctx._chunks.append(c)
+            out.append(c)
+        return out
+
+    def size_chunks_up(self):
+        return int(self.ctx._lib.cioa_stream_size_chunks_up(self._h))
+
+
+class Chunk:
+    """cio_chunk over the C layer."""
+
+    def __init__(self, ctx, h):
+        self.ctx, self._h, self._lib = ctx, h, ctx._lib
+
+    def _c(self):
+        if not self._h:
+            raise ValueError("chunk is closed")
+        return self._h
+
+    @property
+    def name(self):
+        return self._lib.cioa_chunk_name(self._c()).decode()
 
     def write(self, data):
-        """cio_file_write (src/cio_file.c:994-1073)."""
-        data = bytes(data)
-        if not data:
-            return 0
-        if self.map is None:
-            return -1
-        meta = self.meta_len()
-        av = self.alloc_size - HDR_MIN - meta - self.data_size
-        if av < len(data):
-            pre = HDR_MIN + meta
-            new_size = self.alloc_size + self.realloc_size
-            while new_size < pre + self.data_size + len(data):
-                new_size += self.realloc_size
-            self._resize(_round_up(new_size, PAGE))
-        if self.crc_reset:
-            self._set_content_len(self.data_size)
-        if self.flags & CIO_CHECKSUM and self.deferred_crc:
-            if self.crc_reset:                       # full recompute at the sync
-                self.crc_cur, self.crc_end = CRC_INIT, CONTENT_OFFSET
-                self.crc_reset = False
-        elif self.flags & CIO_CHECKSUM:
-            if self.crc_reset:                       # update_checksum (:103-108)
-                self.crc_cur = self._region_crc()
-                self.crc_reset = False
-            self.crc_cur = crc_update(self.crc_cur, data)
-            self.map[2:10] = struct.pack("<Q", self.crc_cur)   # raw 8-byte crc_t (:111)
-            self.crc_end = HDR_MIN + meta + self.data_size + len(data)
-        off = HDR_MIN + meta + self.data_size
-        self.map[off:off + len(data)] = data
-        self.data_size += len(data)
-        self.synced = False
-        self._set_content_len(self.data_size)
-        self.taint = True
-        return 0
+        b = bytes(data)
+        return int(self._lib.cioa_chunk_write(self._c(), b, len(b)))
 
     def write_at(self, data, offset):
-        """cio_chunk_write_at (src/cio_chunk.c:184-209)."""
-        self.data_size = offset
-        self.crc_reset = True
-        return self.write(data)
+        b = bytes(data)
+        return int(self._lib.cioa_chunk_write_at(self._c(), int(offset), b, len(b)))
 
-    def write_metadata(self, meta):
-        """cio_file_write_metadata + adjust_layout (src/cio_file.c:1075-1145, 130-146)."""
-        meta = bytes(meta)
-        cur_meta = self.meta_len()
-        content = bytes(self.map[HDR_MIN + cur_meta:HDR_MIN + cur_meta + self.data_size])
-        need = HDR_MIN + len(meta) + self.data_size
-        if cur_meta < len(meta) and self.alloc_size < need:
-            self._resize(need)
-        self.map[HDR_MIN:HDR_MIN + len(meta)] = meta
-        self.map[HDR_MIN + len(meta):HDR_MIN + len(meta) + self.data_size] = content
-        self.map[CONTENT_OFFSET:CONTENT_OFFSET + 2] = struct.pack(">H", len(meta))
-        if self.flags & CIO_CHECKSUM and self.deferred_crc:
-            self.crc_cur, self.crc_end = CRC_INIT, CONTENT_OFFSET
-        elif self.flags & CIO_CHECKSUM:
-            self.crc_cur = self._region_crc()
-            self.crc_end = HDR_MIN + len(meta) + self.data_size
-        self.synced = False
-        return 0
+    def meta_write(self, meta):
+        b = bytes(meta)
+        return int(self._lib.cioa_meta_write(self._c(), b, len(b)))
+
+    write_metadata = meta_write
+
+    def meta_len(self):
+        return int(self._lib.cioa_meta_size(self._c()))
 
     def sync(self):
-        """cio_file_sync (src/cio_file.c:1147-1250) without trimming."""
-        if self.map is None or self.synced or not (self.flags & CIO_OPEN):
-            return 0
-        if self.deferred_crc and self.flags & CIO_CHECKSUM:
-            return sync_batch([self])
-        if self.flags & CIO_CHECKSUM:
-            fin = (self.crc_cur ^ 0xFFFFFFFF) & 0xFFFFFFFF
-            self.map[2:10] = struct.pack("<Q", int.from_bytes(struct.pack(">I", fin), "little"))
-        self.map.flush()
-        self.synced = True
-        self.fs_size = os.fstat(self.fd).st_size
-        return 0
+        return int(self._lib.cioa_chunk_sync(self._c()))
+
+    def up(self):
+        return int(self._lib.cioa_chunk_up(self._c()))
+
+    def up_force(self):
+        return int(self._lib.cioa_chunk_up_force(self._c()))
+
+    def down(self):
+        return int(self._lib.cioa_chunk_down(self._c()))
+
+    def is_up(self):
+        return bool(self._lib.cioa_chunk_is_up(self._c()))
+
+    def lock(self):
+        return int(self._lib.cioa_chunk_lock(self._c()))
+
+    def unlock(self):
+        return int(self._lib.cioa_chunk_unlock(self._c()))
+
+    def tx_begin(self):
+        return int(self._lib.cioa_chunk_tx_begin(self._c()))
+
+    def tx_commit(self):
+        return int(self._lib.cioa_chunk_tx_commit(self._c()))
+
+    def tx_rollback(self):
+        return int(self._lib.cioa_chunk_tx_rollback(self._c()))
+
+    @property
+    def error(self):
+        return int(self._lib.cioa_error_get(self._c()))
+
+    @property
+    def data_size(self):
+        return int(self._lib.cioa_chunk_get_content_size(self._c()))
+
+    @property
+    def real_size(self):
+        return int(self._lib.cioa_chunk_get_real_size(self._c()))
+
+    @property
+    def crc_cur(self):
+        return int(self._lib.cioa_chunk_crc_cur(self._c()))
+
+    @crc_cur.setter
+    def crc_cur(self, v):
+        self._lib.cioa_chunk_set_crc_cur(self._c(), v & 0xFFFFFFFF)
+
+    @property
+    def map(self):
+        """The chunk's mapping as a ctypes byte array (None when down)."""
+        size = ctypes.c_size_t(0)
+        p = self._lib.cioa_chunk_map(self._c(), ctypes.byref(size))
+        if not p:
+            return None
+        return (ctypes.c_char * size.value).from_address(p)
+
+    @property
+    def alloc_size(self):
+        m = self.map
+        return 0 if m is None else len(m)
+
+    def hash(self):
+        m = self.map
+        return None if m is None else bytes(m[2:6])
+
+    def content(self):
+        m = self.map
+        off = HDR_MIN + self.meta_len()
+        return bytes(m[off:off + self.data_size])
+
+    def close(self, delete=False):
+        if self._h:
+            self._lib.cioa_chunk_close(self._h, 1 if delete else 0)
+            self._h = None
+
+
+def sync_batch(chunks):
+    """cioa_chunk_sync_batch: every chunk's deferred CRC in ONE GPU pass."""
+    chunks = [c for c in chunks if c is not None]
+    if not chunks:
+        return CIO_OK
+    lib = _bind()
+    arr = (ctypes.c_void_p * len(chunks))(*[c._c() for c in chunks])
+    return int(lib.cioa_chunk_sync_batch(arr, len(chunks)))
+
+
+class ChunkFile(Chunk):
+    """One chunk addressed by its path (root/stream/name), in a private context."""
+
+    @classmethod
+    def open(cls, path, flags=CIO_OPEN | CIO_CHECKSUM, deferred_crc=False, ctx_flags=0):
+        path = os.path.abspath(path)
+        stream_dir = os.path.dirname(path)
+        root, stream, name = os.path.dirname(stream_dir), os.path.basename(stream_dir), os.path.basename(path)
+        cflags = (flags & (CIO_CHECKSUM | CIO_FULL_SYNC | CIO_TRIM_FILES)) | ctx_flags
+        if deferred_crc:
+            cflags |= CIOA_DEFERRED_CRC
+        ctx = Context(root, cflags | (flags & (CIO_OPEN | CIO_OPEN_RD)))
+        st = ctx.stream(stream)
+        c, err = st.open(name, (flags & (CIO_OPEN | CIO_OPEN_RD)) or CIO_OPEN)
+        if c is None:
+            cf = cls.__new__(cls)
+            cf.ctx, cf._h, cf._lib, cf.path = ctx, None, ctx._lib, path
+            cf._open_error = ctx.last_chunk_error
+            return cf, err
+        cf = cls(ctx, c._h)
+        ctx._chunks[-1] = cf
+        cf.path = path
+        return cf, CIO_OK
+
+    @property
+    def error(self):
+        if not self._h:
+            return getattr(self, "_open_error", 0)
+        return super().error
+
+    def close(self, delete=False):
+        super().close(delete)
+        self.ctx.close()
+
+
+def perf_write(root, data, files=1000, writes=5, batch=100, flags=CIO_CHECKSUM | CIOA_DEFERRED_CRC):
+    """BASELINE config 1's loop through the C layer (cioa_bench_perf_write):
+    (seconds, bytes)."""
+    lib = _bind()
+    buf = np.frombuffer(bytes(data), np.uint8)
+    secs, nb = ctypes.c_double(0), ctypes.c_uint64(0)
+    rc = lib.cioa_bench_perf_write(os.fsencode(root), buf.ctypes.data, buf.size, files, writes, batch, flags,
+                                   ctypes.byref(secs), ctypes.byref(nb))
+    if rc != CIO_OK:
+        raise _lib.CioGpuError(f"cioa_bench_perf_write failed: {_lib.lib().cio_gpu_last_error().decode()}")
+    return secs.value, int(nb.value)
+
+
+def header_crc_be(path):
+    with open(path, "rb") as f:
+        return struct.unpack(">I", f.read(6)[2:6])[0]

@@ -153,8 +153,10 @@ def crc32_batch_dev(base, offs, lens, seeds=None, stream=None):
     return _to_u32_numpy(out)
 
 
-def crc32_batch_host(bufs, seeds=None):
-    """Raw CRC states of host buffers via pinned staging + H2D + GPU kernels."""
+def crc32_batch_host(bufs, seeds=None, devices=None):
+    """Raw CRC states of host buffers via pinned staging + H2D + GPU kernels.
+    devices: GPU ordinals to spread the batch over (chunk i -> devices[i %
+    len]); None = the current device."""
     arrays = [_as_bytes(b) for b in bufs]
     n = len(arrays)
     ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data if a.size else None for a in arrays])
@@ -164,10 +166,21 @@ def crc32_batch_host(bufs, seeds=None):
     if seeds is not None:
         seeds_arr = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint32))
         seeds_p = seeds_arr.ctypes.data_as(_lib.c_u32_p)
+    if devices:
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _lib.check(_lib.lib().cio_crc32_batch_host_multi(ptrs, lens, seeds_p, out.ctypes.data_as(_lib.c_u32_p),
+                                                         n, devs, len(devices)),
+                   "cio_crc32_batch_host_multi")
+        return out[:n]
     _lib.check(_lib.lib().cio_crc32_batch_host(ptrs, lens, seeds_p,
                                                out.ctypes.data_as(_lib.c_u32_p), n),
                "cio_crc32_batch_host")
     return out[:n]
+
+
+def device_count():
+    """Visible GPUs (cio_gpu_device_count)."""
+    return int(_lib.lib().cio_gpu_device_count())
 
 
 def host_register(arr):

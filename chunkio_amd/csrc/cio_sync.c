@@ -16,13 +16,9 @@
 #include "chunkio_amd/cio_crc32_gpu.h"
 #include "chunkio_amd/cio_verify.h"
 #include "chunkio_amd/cio_sync.h"
+#include "cio_layout.h"
 
-/* On-disk layout, include/chunkio/cio_file_st.h:151-157 */
-#define HDR_MIN               24
-#define HDR_CONTENT_OFFSET    22
-#define HDR_CONTENT_LEN_OFF   10
-
-int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags)
+int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev)
 {
     const void **bufs = NULL;
     size_t *lens = NULL, *idx = NULL, m = 0;
@@ -47,16 +43,15 @@ int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags)
     for (size_t i = 0; i < n; i++) {
         cio_sync_item *it = &items[i];
         it->status = CIO_OK;
-        if (!it->map || it->fs_size < HDR_MIN || it->map[0] != 0xc1 || it->map[1] != 0x00) {
+        if (!it->map || it->fs_size < CIOA_HDR_MIN || it->map[0] != CIOA_HDR_ID_00 ||
+            it->map[1] != CIOA_HDR_ID_01) {
             it->status = CIO_CORRUPTED;
             continue;
         }
-        const unsigned char *b = it->map + HDR_CONTENT_LEN_OFF;
-        const uint64_t clen = ((uint64_t) b[0] << 24) | ((uint64_t) b[1] << 16) |
-                              ((uint64_t) b[2] << 8) | b[3];
-        const uint64_t meta = ((uint64_t) it->map[HDR_CONTENT_OFFSET] << 8) | it->map[HDR_CONTENT_OFFSET + 1];
-        const uint64_t end = HDR_MIN + meta + clen;
-        if (end > it->fs_size || it->crc_end < HDR_CONTENT_OFFSET || it->crc_end > end) {
+        const uint64_t clen = cioa_st_get_content_len_field(it->map);
+        const uint64_t meta = cioa_st_meta_len(it->map);
+        const uint64_t end = it->data_end ? it->data_end : CIOA_HDR_MIN + meta + clen;
+        if (end > it->fs_size || it->crc_end < CIOA_HDR_CONTENT_OFFSET || it->crc_end > end) {
             it->status = CIO_CORRUPTED;
             continue;
         }
@@ -67,7 +62,7 @@ int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags)
         it->crc_end = end;      /* committed below, after the batch ran */
         m++;
     }
-    if (m > 0 && cio_crc32_batch_host(bufs, lens, seeds, raw, m) != CIO_OK) {
+    if (m > 0 && cio_crc32_batch_host_multi(bufs, lens, seeds, raw, m, devices, ndev) != CIO_OK) {
         /* restore the ranges: nothing was written */
         for (size_t k = 0; k < m; k++) {
             items[idx[k]].crc_end = (uint64_t) ((const unsigned char *) bufs[k] - items[idx[k]].map);
@@ -85,8 +80,12 @@ int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags)
             v = (crc_t) raw[k];                                   /* update_checksum :111 */
         }
         memcpy(it->map + 2, &v, sizeof(v));
-        if (flags & CIOA_SYNC_MSYNC) {
-            (void) msync(it->map, it->fs_size, MS_ASYNC);
+        /* cio_file_native_sync (src/cio_file_unix.c:477-497): MS_SYNC under
+         * CIO_FULL_SYNC, else MS_ASYNC; a failed msync fails the sync
+         * (cio_file.c:1231-1236), the chunk stays unsynced. */
+        if ((flags & (CIOA_SYNC_MSYNC | CIOA_SYNC_FULL)) &&
+            msync(it->map, it->fs_size, (flags & CIOA_SYNC_FULL) ? MS_SYNC : MS_ASYNC) != 0) {
+            it->status = CIO_ERROR;
         }
     }
 out:
@@ -96,4 +95,9 @@ out:
     free(seeds);
     free(raw);
     return rc;
+}
+
+int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags)
+{
+    return cio_file_sync_batch_multi(items, n, flags, NULL, 0);
 }

@@ -1,0 +1,1496 @@
+/*
+ * cioa_chunk.c -- chunkio's filesystem chunk layer in C over the batched GPU
+ * CRC path (see include/chunkio_amd/cioa_chunk.h for the API map).
+ *
+ * The state kept per chunk is the reference's struct cio_file
+ * (include/chunkio/cio_file.h:31-55) plus, for CIOA_DEFERRED_CRC, crc_end:
+ * the file offset up to which crc_cur is current.  Immediate mode follows
+ * src/cio_file.c call for call; deferred mode only moves the CRC work:
+ *
+ *   reference                          deferred
+ *   write: crc_update(crc_cur, buf)    write: copy only
+ *          + raw state at map+2
+ *   write_at / metadata: recompute     crc_cur = init, crc_end = 22 (recomputed
+ *                                      at once where the legacy length inference
+ *                                      makes the reference hash more than the data)
+ *   sync: finalize crc_cur             sync: crc_update(crc_cur, map[crc_end..end))
+ *                                            on the GPU, then finalize (batched
+ *                                            over many chunks by sync_batch)
+ *   tx_begin: tx_crc = crc_cur         bring crc_cur up to date first (GPU), then
+ *                                      the same; rollback also resets crc_end
+ *
+ * so the bytes on disk after every sync are the reference's.
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <dirent.h>
+#include <time.h>
+#include <unistd.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <arpa/inet.h>
+
+#include <crc32/crc32.h>
+#include "chunkio_amd/cio_crc32_gpu.h"
+#include "chunkio_amd/cio_verify.h"
+#include "chunkio_amd/cio_sync.h"
+#include "chunkio_amd/cioa_chunk.h"
+#include "cio_layout.h"
+
+#define CIOA_REALLOC_HINT_MAX (8 * 1000 * 1000)   /* chunkio.h:60 */
+#define ROUND_UP(N, S) ((((N) + (S) - 1) / (S)) * (S))
+
+struct cioa_ctx {
+    char *root;
+    int flags;
+    long page;
+    size_t realloc_hint;         /* 0: page * 8 (CIO_REALLOC_HINT_MIN) */
+    size_t max_up, total, total_up;
+    int last_chunk_error;
+    int *devs;
+    int ndev;
+    cioa_stream *streams;
+};
+
+struct cioa_stream {
+    char *name;
+    cioa_ctx *ctx;
+    cioa_chunk *head, *tail;
+    cioa_stream *next;
+};
+
+struct cioa_chunk {
+    char *name;
+    char *path;
+    cioa_ctx *ctx;
+    cioa_stream *st;
+    cioa_chunk *prev, *next;
+    /* struct cio_file */
+    int flags;
+    int fd;
+    unsigned char *map;
+    size_t alloc_size, fs_size, data_size, realloc_size;
+    uint32_t crc_cur;
+    int crc_reset, taint, synced;
+    uint64_t crc_end;            /* deferred mode */
+    /* struct cio_chunk */
+    int lock;
+    int tx_active;
+    uint32_t tx_crc;             /* uint32_t as in cio_chunk.h:35 */
+    size_t tx_content_length;
+    int error_n;
+};
+
+static int deferred(const cioa_chunk *ch)
+{
+    return (ch->ctx->flags & (CIOA_DEFERRED_CRC | CIO_CHECKSUM)) == (CIOA_DEFERRED_CRC | CIO_CHECKSUM);
+}
+
+static void error_set(cioa_chunk *ch, int err)
+{
+    ch->error_n = err;
+    ch->ctx->last_chunk_error = err;
+}
+
+static int mkpath(const char *path)
+{
+    char tmp[4096];
+    size_t n = strlen(path);
+    if (n == 0 || n >= sizeof(tmp)) {
+        return -1;
+    }
+    memcpy(tmp, path, n + 1);
+    for (char *p = tmp + 1; *p; p++) {
+        if (*p == '/') {
+            *p = '\0';
+            if (mkdir(tmp, 0755) != 0 && errno != EEXIST) {
+                return -1;
+            }
+            *p = '/';
+        }
+    }
+    if (mkdir(tmp, 0755) != 0 && errno != EEXIST) {
+        return -1;
+    }
+    return 0;
+}
+
+/* ---- natives (src/cio_file_unix.c) --------------------------------------- */
+
+static int native_is_open(const cioa_chunk *ch)
+{
+    return ch->fd >= 0;
+}
+
+static int native_open(cioa_chunk *ch)             /* :396-417 */
+{
+    if (ch->fd >= 0) {
+        return CIO_OK;
+    }
+    if (ch->flags & CIO_OPEN_RW) {
+        ch->fd = open(ch->path, O_RDWR | O_CREAT, (mode_t) 0600);
+    }
+    else if (ch->flags & CIO_OPEN_RD) {
+        ch->fd = open(ch->path, O_RDONLY);
+    }
+    return ch->fd == -1 ? CIO_ERROR : CIO_OK;
+}
+
+static int native_close(cioa_chunk *ch)
+{
+    if (ch->fd >= 0) {
+        close(ch->fd);
+        ch->fd = -1;
+    }
+    return CIO_OK;
+}
+
+static int native_get_size(cioa_chunk *ch, size_t *size)   /* :317-341 */
+{
+    struct stat sb;
+    int r = ch->fd >= 0 ? fstat(ch->fd, &sb) : stat(ch->path, &sb);
+    if (r != 0) {
+        return CIO_ERROR;
+    }
+    *size = (size_t) sb.st_size;
+    return CIO_OK;
+}
+
+static int update_size(cioa_chunk *ch)                      /* cio_file.c:906-917 */
+{
+    if (native_get_size(ch, &ch->fs_size) != CIO_OK) {
+        ch->fs_size = 0;
+        return CIO_ERROR;
+    }
+    return CIO_OK;
+}
+
+static int native_map(cioa_chunk *ch, size_t size, int populate)   /* :74-111 */
+{
+    int prot;
+    if (ch->fd < 0) {
+        return CIO_ERROR;
+    }
+    if (ch->map) {
+        return CIO_OK;
+    }
+    if (ch->flags & CIO_OPEN_RW) {
+        prot = PROT_READ | PROT_WRITE;
+    }
+    else if (ch->flags & CIO_OPEN_RD) {
+        prot = PROT_READ;
+    }
+    else {
+        return CIO_ERROR;
+    }
+    void *p = mmap(NULL, size, prot, MAP_SHARED | (populate ? MAP_POPULATE : 0), ch->fd, 0);
+    if (p == MAP_FAILED) {
+        return CIO_ERROR;
+    }
+    ch->map = p;
+    ch->alloc_size = size;
+    return CIO_OK;
+}
+
+static int native_unmap(cioa_chunk *ch)                      /* :47-72 */
+{
+    if (!ch->map) {
+        return CIO_OK;
+    }
+    if (munmap(ch->map, ch->alloc_size) != 0) {
+        return CIO_ERROR;
+    }
+    ch->alloc_size = 0;
+    ch->map = NULL;
+    return CIO_OK;
+}
+
+static int native_resize(cioa_chunk *ch, size_t new_size)    /* :499-571 */
+{
+    int r;
+    if (new_size > ch->fs_size) {
+        /* fallocate: a full filesystem fails here (ENOSPC), not as a SIGBUS
+         * on the first store into the mapping */
+        r = fallocate(ch->fd, 0, 0, (off_t) new_size);
+        if (r == -1 && errno == EOPNOTSUPP) {
+            r = posix_fallocate(ch->fd, 0, (off_t) new_size);
+        }
+    }
+    else {
+        r = ftruncate(ch->fd, (off_t) new_size);
+    }
+    if (r == 0) {
+        ch->fs_size = new_size;
+    }
+    return r == 0 ? CIO_OK : CIO_ERROR;
+}
+
+static int file_resize(cioa_chunk *ch, size_t new_size)      /* cio_file.c:1252-1302 */
+{
+    if (native_resize(ch, new_size) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    if (ch->map) {
+        void *p = mremap(ch->map, ch->alloc_size, new_size, MREMAP_MAYMOVE);
+        if (p == MAP_FAILED) {
+            return CIO_ERROR;
+        }
+        ch->map = p;
+        ch->alloc_size = new_size;
+    }
+    return CIO_OK;
+}
+
+/* ---- CRC helpers ----------------------------------------------------------- */
+
+static uint64_t region_end(const cioa_chunk *ch)
+{
+    return CIOA_HDR_MIN + (uint64_t) cioa_st_meta_len(ch->map) + ch->data_size;
+}
+
+/* cio_file_calculate_checksum (cio_file.c:66-94): crc_update(crc_cur,
+ * map + 22, 2 + meta_len + content_len), on the GPU. */
+static int calculate_checksum(cioa_chunk *ch, uint32_t *out)
+{
+    if (ch->fs_size == 0) {
+        update_size(ch);
+    }
+    const int64_t clen = cioa_st_content_len(ch->map, ch->fs_size, ch->taint,
+                                             (ch->flags & CIO_OPEN_RW) != 0);
+    const void *buf = ch->map + CIOA_HDR_CONTENT_OFFSET;
+    size_t len = 2 + (size_t) cioa_st_meta_len(ch->map) + (clen > 0 ? (size_t) clen : 0);
+    uint32_t seed = ch->crc_cur;
+    return cio_crc32_batch_host_multi(&buf, &len, &seed, out, 1, ch->ctx->devs, ch->ctx->ndev);
+}
+
+/* Would cio_file_calculate_checksum run the legacy length inference now
+ * (cio_file_st.h:166-176: untainted chunk, zero length field, non-zero first
+ * content byte)?  Then its CRC covers the inferred region, not the data. */
+static int legacy_inference_due(cioa_chunk *ch)
+{
+    if (ch->taint || cioa_st_get_content_len_field(ch->map) != 0) {
+        return 0;
+    }
+    if (ch->fs_size == 0) {
+        update_size(ch);
+    }
+    const size_t content_offset = CIOA_HDR_MIN + (size_t) cioa_st_meta_len(ch->map);
+    return ch->fs_size > content_offset && content_offset < ch->alloc_size && ch->map[content_offset] != 0;
+}
+
+/* Full recompute (write_at reset, metadata move).  Immediate mode, and the
+ * deferred mode when the legacy inference would make the reference hash
+ * more than the data: crc_update(init, region) now, on the GPU.  Otherwise
+ * (deferred) the recompute folds into the next sync: crc_end = 22. */
+static int full_recompute(cioa_chunk *ch)
+{
+    ch->crc_cur = 0xffffffffu;
+    if (ch->fs_size == 0) {
+        update_size(ch);                 /* as cio_file_calculate_checksum does (:73-75) */
+    }
+    if (deferred(ch) && !legacy_inference_due(ch)) {
+        ch->crc_end = CIOA_HDR_CONTENT_OFFSET;
+        return CIO_OK;
+    }
+    uint32_t tmp;
+    if (calculate_checksum(ch, &tmp) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    ch->crc_cur = tmp;
+    /* crc_cur is the reference's crc_cur as of the current end of data */
+    ch->crc_end = region_end(ch);
+    return CIO_OK;
+}
+
+/* Deferred mode: bring crc_cur up to the current end of data (GPU) and leave
+ * the raw state at map+2, as update_checksum would have (cio_file.c:111). */
+static int catch_up(cioa_chunk *ch)
+{
+    if (!deferred(ch) || !ch->map) {
+        return CIO_OK;
+    }
+    if (ch->crc_reset) {
+        if (full_recompute(ch) != CIO_OK) {
+            return CIO_ERROR;
+        }
+        ch->crc_reset = 0;
+    }
+    cio_sync_item it = {0};
+    it.map = ch->map;
+    it.fs_size = ch->alloc_size;
+    it.crc_end = ch->crc_end;
+    it.crc_cur = ch->crc_cur;
+    it.data_end = region_end(ch);
+    if (it.crc_end == it.data_end) {
+        return CIO_OK;
+    }
+    if (cio_file_sync_batch_multi(&it, 1, 0, ch->ctx->devs, ch->ctx->ndev) != CIO_OK ||
+        it.status != CIO_OK) {
+        return CIO_ERROR;
+    }
+    ch->crc_cur = it.crc_cur;
+    ch->crc_end = it.crc_end;
+    return CIO_OK;
+}
+
+/* ---- mapping, format check (cio_file.c:187-294, 345-493) ----------------- */
+
+/* Everything of mmap_file up to the CRC: size, resize/init of an empty file,
+ * map, content length.  Returns CIO_OK (ready for the CRC verify, or fully
+ * set up when the file was empty), CIO_ERROR or CIO_CORRUPTED. */
+static int map_prepare(cioa_chunk *ch, size_t size, int *fresh)
+{
+    size_t fs_size = 0;
+    *fresh = 0;
+    if (ch->map) {
+        return CIO_OK;
+    }
+    ch->taint = 0;
+    if (size > 0) {
+        fs_size = size;
+    }
+    else if (native_get_size(ch, &fs_size) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    if (fs_size > 0) {
+        size = fs_size;
+        ch->synced = 1;
+    }
+    else {
+        if ((ch->flags & CIO_OPEN_RW) == 0) {
+            error_set(ch, CIO_ERR_PERMISSION);
+            return CIO_CORRUPTED;
+        }
+        ch->synced = 0;
+        if (size < CIOA_HDR_MIN) {
+            size += CIOA_HDR_MIN;
+        }
+        size = ROUND_UP(size, (size_t) ch->ctx->page);
+        if (file_resize(ch, size) != CIO_OK) {
+            return CIO_ERROR;
+        }
+    }
+    if (native_map(ch, size, fs_size > 0) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    if (fs_size > 0) {
+        const int64_t clen = cioa_st_content_len(ch->map, fs_size, ch->taint,
+                                                 (ch->flags & CIO_OPEN_RW) != 0);
+        if (clen == -1) {
+            error_set(ch, CIO_ERR_BAD_FILE_SIZE);
+            native_unmap(ch);
+            ch->data_size = 0;
+            ch->alloc_size = 0;
+            return CIO_CORRUPTED;
+        }
+        ch->data_size = (size_t) clen;
+        ch->fs_size = fs_size;
+        return CIO_OK;
+    }
+    /* cio_file_format_check, new file (:202-227) */
+    ch->data_size = 0;
+    ch->fs_size = 0;
+    if (ch->alloc_size < CIOA_HDR_MIN) {
+        error_set(ch, CIO_ERR_BAD_LAYOUT);
+        native_unmap(ch);
+        return CIO_CORRUPTED;
+    }
+    cioa_write_init_header(ch->map, (ch->ctx->flags & CIO_CHECKSUM) != 0);
+    if (ch->ctx->flags & CIO_CHECKSUM) {
+        if (deferred(ch)) {
+            ch->crc_end = CIOA_HDR_CONTENT_OFFSET;
+        }
+        else {
+            /* calculate_checksum over the two meta-length bytes */
+            ch->crc_cur = (uint32_t) crc_update(ch->crc_cur, ch->map + CIOA_HDR_CONTENT_OFFSET, 2);
+        }
+    }
+    *fresh = 1;
+    return CIO_OK;
+}
+
+/* The verdict of the verify pass for one prepared chunk. */
+static int map_finish(cioa_chunk *ch, const cio_verify_item *it)
+{
+    if (it->status != CIO_OK) {
+        error_set(ch, it->error);
+        native_unmap(ch);
+        ch->data_size = 0;
+        return CIO_CORRUPTED;
+    }
+    if (ch->ctx->flags & CIO_CHECKSUM) {
+        ch->crc_cur = it->crc_raw;
+        ch->crc_end = region_end(ch);
+    }
+    ch->ctx->total_up++;
+    return CIO_OK;
+}
+
+static int verify_flags(const cioa_chunk *ch)
+{
+    return (ch->ctx->flags & CIO_CHECKSUM ? CIOA_VERIFY_CHECKSUM : 0) |
+           (ch->flags & CIO_OPEN_RW ? CIOA_VERIFY_WRITEBACK : 0);
+}
+
+static int mmap_file(cioa_chunk *ch, size_t size)
+{
+    int fresh;
+    if (ch->map) {
+        return CIO_OK;
+    }
+    int ret = map_prepare(ch, size, &fresh);
+    if (ret != CIO_OK) {
+        return ret;
+    }
+    if (fresh) {
+        ch->ctx->total_up++;
+        return CIO_OK;
+    }
+    cio_verify_item it = {0};
+    it.map = ch->map;
+    it.fs_size = ch->fs_size;
+    it.taint = ch->taint;
+    if (cio_file_verify_batch_multi(&it, 1, verify_flags(ch), ch->ctx->devs, ch->ctx->ndev) != CIO_OK) {
+        native_unmap(ch);
+        ch->data_size = 0;
+        return CIO_ERROR;
+    }
+    return map_finish(ch, &it);
+}
+
+/* ---- context / streams ----------------------------------------------------- */
+
+cioa_ctx *cioa_create(const char *root_path, int flags)
+{
+    if (!root_path || !*root_path) {
+        return NULL;
+    }
+    if (mkpath(root_path) != 0) {
+        return NULL;
+    }
+    cioa_ctx *ctx = calloc(1, sizeof(*ctx));
+    if (!ctx) {
+        return NULL;
+    }
+    ctx->root = strdup(root_path);
+    /* sanitize chunk open flags (src/chunkio.c:103-105) */
+    if (!(flags & CIO_OPEN_RW) && !(flags & CIO_OPEN_RD)) {
+        flags |= CIO_OPEN_RW;
+    }
+    ctx->flags = flags;
+    ctx->page = sysconf(_SC_PAGESIZE);
+    ctx->max_up = CIOA_MAX_CHUNKS_UP;
+    return ctx;
+}
+
+static void stream_destroy(cioa_stream *st)
+{
+    while (st->head) {
+        cioa_chunk_close(st->head, 0);
+    }
+    free(st->name);
+    free(st);
+}
+
+void cioa_destroy(cioa_ctx *ctx)
+{
+    if (!ctx) {
+        return;
+    }
+    while (ctx->streams) {
+        cioa_stream *st = ctx->streams;
+        ctx->streams = st->next;
+        stream_destroy(st);
+    }
+    free(ctx->devs);
+    free(ctx->root);
+    free(ctx);
+}
+
+int cioa_set_max_chunks_up(cioa_ctx *ctx, int n)
+{
+    if (n < 1) {
+        return -1;
+    }
+    ctx->max_up = (size_t) n;
+    return 0;
+}
+
+int cioa_set_realloc_size_hint(cioa_ctx *ctx, size_t hint)
+{
+    if (hint < (size_t) ctx->page * 8 || hint > CIOA_REALLOC_HINT_MAX) {
+        return -1;
+    }
+    ctx->realloc_hint = hint;
+    return 0;
+}
+
+void cioa_enable_file_trimming(cioa_ctx *ctx)
+{
+    ctx->flags |= CIO_TRIM_FILES;
+}
+
+void cioa_disable_file_trimming(cioa_ctx *ctx)
+{
+    ctx->flags &= ~CIO_TRIM_FILES;
+}
+
+int cioa_get_flags(const cioa_ctx *ctx)
+{
+    return ctx->flags;
+}
+
+int cioa_set_devices(cioa_ctx *ctx, const int *devices, int n)
+{
+    free(ctx->devs);
+    ctx->devs = NULL;
+    ctx->ndev = 0;
+    if (n <= 0) {
+        return CIO_OK;
+    }
+    ctx->devs = malloc((size_t) n * sizeof(int));
+    if (!ctx->devs) {
+        return CIO_ERROR;
+    }
+    memcpy(ctx->devs, devices, (size_t) n * sizeof(int));
+    ctx->ndev = n;
+    return CIO_OK;
+}
+
+int cioa_last_chunk_error(const cioa_ctx *ctx)
+{
+    return ctx->last_chunk_error;
+}
+
+size_t cioa_total_chunks(const cioa_ctx *ctx)
+{
+    return ctx->total;
+}
+
+size_t cioa_total_chunks_up(const cioa_ctx *ctx)
+{
+    return ctx->total_up;
+}
+
+cioa_stream *cioa_stream_get(cioa_ctx *ctx, const char *name)
+{
+    for (cioa_stream *st = ctx->streams; st; st = st->next) {
+        if (strcmp(st->name, name) == 0) {
+            return st;
+        }
+    }
+    return NULL;
+}
+
+cioa_stream *cioa_stream_create(cioa_ctx *ctx, const char *name)
+{
+    char path[4096];
+    if (!ctx || !name) {
+        return NULL;
+    }
+    const size_t len = strlen(name);
+    if (len == 0 || (len == 1 && (name[0] == '.' || name[0] == '/'))) {
+        return NULL;
+    }
+    if (cioa_stream_get(ctx, name)) {
+        return NULL;
+    }
+    if (snprintf(path, sizeof(path), "%s/%s", ctx->root, name) >= (int) sizeof(path) ||
+        mkpath(path) != 0 || access(path, W_OK) != 0) {
+        return NULL;
+    }
+    cioa_stream *st = calloc(1, sizeof(*st));
+    if (!st) {
+        return NULL;
+    }
+    st->name = strdup(name);
+    st->ctx = ctx;
+    st->next = ctx->streams;
+    ctx->streams = st;
+    return st;
+}
+
+size_t cioa_stream_size_chunks_up(cioa_stream *st)
+{
+    size_t total = 0;
+    for (cioa_chunk *ch = st->head; ch; ch = ch->next) {
+        if (cioa_chunk_is_up(ch)) {
+            total += ch->data_size;
+        }
+    }
+    return total;
+}
+
+size_t cioa_stream_chunks(cioa_stream *st, cioa_chunk **out, size_t cap)
+{
+    size_t k = 0;
+    for (cioa_chunk *ch = st->head; ch; ch = ch->next, k++) {
+        if (k < cap) {
+            out[k] = ch;
+        }
+    }
+    return k;
+}
+
+/* ---- chunk open / close ------------------------------------------------------ */
+
+static cioa_chunk *chunk_new(cioa_ctx *ctx, cioa_stream *st, const char *name, int flags)
+{
+    char path[4096];
+    if (strchr(name, '/') ||
+        snprintf(path, sizeof(path), "%s/%s/%s", ctx->root, st->name, name) >= (int) sizeof(path)) {
+        return NULL;
+    }
+    cioa_chunk *ch = calloc(1, sizeof(*ch));
+    if (!ch) {
+        return NULL;
+    }
+    ch->name = strdup(name);
+    ch->path = strdup(path);
+    ch->ctx = ctx;
+    ch->st = st;
+    ch->fd = -1;
+    ch->flags = flags;
+    ch->realloc_size = ctx->realloc_hint ? ctx->realloc_hint : (size_t) ctx->page * 8;
+    ch->crc_cur = 0xffffffffu;
+    ch->crc_end = CIOA_HDR_CONTENT_OFFSET;
+    return ch;
+}
+
+static void chunk_link(cioa_chunk *ch)
+{
+    cioa_stream *st = ch->st;
+    ch->prev = st->tail;
+    ch->next = NULL;
+    if (st->tail) {
+        st->tail->next = ch;
+    }
+    else {
+        st->head = ch;
+    }
+    st->tail = ch;
+    ch->ctx->total++;
+}
+
+static void chunk_free(cioa_chunk *ch)
+{
+    free(ch->name);
+    free(ch->path);
+    free(ch);
+}
+
+cioa_chunk *cioa_chunk_open(cioa_ctx *ctx, cioa_stream *st, const char *name, int flags, size_t size,
+                            int *err)
+{
+    (void) size;                               /* ignored, as cio_file.c:648 does */
+    int dummy;
+    if (!err) {
+        err = &dummy;
+    }
+    if (!ctx || !st || !name || !*name) {
+        return NULL;
+    }
+    cioa_chunk *ch = chunk_new(ctx, st, name, flags);
+    if (!ch) {
+        return NULL;
+    }
+    /* open_and_up (cio_file.c:564-571, 701-715): over the limit the chunk
+     * is registered down */
+    if (ctx->total_up >= ctx->max_up) {
+        update_size(ch);
+        *err = CIO_OK;
+        chunk_link(ch);
+        return ch;
+    }
+    int ret = native_open(ch);
+    if (ret != CIO_OK || update_size(ch) != CIO_OK) {
+        native_close(ch);
+        chunk_free(ch);
+        *err = CIO_ERROR;
+        return NULL;
+    }
+    ret = mmap_file(ch, ch->fs_size);
+    if (ret == CIO_ERROR || ret == CIO_CORRUPTED || ret == CIO_RETRY) {
+        native_close(ch);
+        chunk_free(ch);
+        *err = ret;
+        return NULL;
+    }
+    *err = CIO_OK;
+    chunk_link(ch);
+    return ch;
+}
+
+static int munmap_file(cioa_chunk *ch)                       /* cio_file.c:300-339 */
+{
+    if (!ch->map) {
+        return -1;
+    }
+    if (!ch->synced) {
+        (void) cioa_chunk_sync(ch);
+    }
+    if (native_unmap(ch) != CIO_OK) {
+        return -1;
+    }
+    ch->data_size = 0;
+    ch->alloc_size = 0;
+    ch->ctx->total_up--;
+    return 0;
+}
+
+void cioa_chunk_close(cioa_chunk *ch, int delete_file)
+{
+    if (!ch) {
+        return;
+    }
+    munmap_file(ch);
+    native_close(ch);
+    if (delete_file) {
+        (void) unlink(ch->path);
+    }
+    cioa_stream *st = ch->st;
+    if (ch->prev) {
+        ch->prev->next = ch->next;
+    }
+    else {
+        st->head = ch->next;
+    }
+    if (ch->next) {
+        ch->next->prev = ch->prev;
+    }
+    else {
+        st->tail = ch->prev;
+    }
+    ch->ctx->total--;
+    chunk_free(ch);
+}
+
+int cioa_chunk_delete(cioa_ctx *ctx, cioa_stream *st, const char *name)
+{
+    char path[4096];
+    if (!ctx || !st || !name || !*name || strchr(name, '/')) {
+        return CIO_ERROR;
+    }
+    snprintf(path, sizeof(path), "%s/%s/%s", ctx->root, st->name, name);
+    return unlink(path) == 0 ? CIO_OK : CIO_ERROR;
+}
+
+/* ---- writes ---------------------------------------------------------------- */
+
+int cioa_chunk_is_up(cioa_chunk *ch)
+{
+    return native_is_open(ch) && ch->map != NULL;
+}
+
+int cioa_chunk_write(cioa_chunk *ch, const void *buf, size_t count)   /* cio_file.c:994-1073 */
+{
+    if (count == 0) {
+        return 0;
+    }
+    if (!ch || !cioa_chunk_is_up(ch)) {
+        return -1;
+    }
+    ch->error_n = 0;
+    const int meta_len = cioa_st_meta_len(ch->map);
+    const size_t av = ch->alloc_size - CIOA_HDR_MIN - (size_t) meta_len - ch->data_size;
+    if (av < count) {
+        const size_t pre = CIOA_HDR_MIN + (size_t) meta_len;
+        size_t new_size = ch->alloc_size + ch->realloc_size;
+        while (new_size < pre + ch->data_size + count) {
+            new_size += ch->realloc_size;
+        }
+        new_size = ROUND_UP(new_size, (size_t) ch->ctx->page);
+        if (file_resize(ch, new_size) != CIO_OK) {
+            return -1;
+        }
+    }
+    if (ch->crc_reset) {
+        cioa_st_set_content_len(ch->map, (uint32_t) ch->data_size);
+    }
+    if (ch->ctx->flags & CIO_CHECKSUM) {
+        /* update_checksum (:97-113): a pending reset recomputes the prefix
+         * from crc_init() (deferred: at the sync) */
+        if (ch->crc_reset) {
+            if (full_recompute(ch) != CIO_OK) {
+                return -1;
+            }
+            ch->crc_reset = 0;
+        }
+        if (!deferred(ch)) {
+            crc_t crc = crc_update((crc_t) ch->crc_cur, buf, count);
+            memcpy(ch->map + 2, &crc, sizeof(crc));
+            ch->crc_cur = (uint32_t) crc;
+        }
+    }
+    memcpy(ch->map + CIOA_HDR_MIN + meta_len + ch->data_size, buf, count);
+    ch->data_size += count;
+    ch->synced = 0;
+    cioa_st_set_content_len(ch->map, (uint32_t) ch->data_size);
+    ch->taint = 1;
+    if (!deferred(ch)) {
+        ch->crc_end = region_end(ch);
+    }
+    return 0;
+}
+
+int cioa_chunk_write_at(cioa_chunk *ch, off_t offset, const void *buf, size_t count)  /* cio_chunk.c:184-209 */
+{
+    if (!ch) {
+        return -1;
+    }
+    ch->error_n = 0;
+    ch->data_size = (size_t) offset;
+    ch->crc_reset = 1;
+    return cioa_chunk_write(ch, buf, count);
+}
+
+static int adjust_layout(cioa_chunk *ch, size_t meta_size)  /* cio_file.c:130-146 */
+{
+    cioa_st_set_meta_len(ch->map, (uint16_t) meta_size);
+    if ((ch->ctx->flags & CIO_CHECKSUM) && full_recompute(ch) != CIO_OK) {
+        return -1;
+    }
+    ch->synced = 0;
+    return 0;
+}
+
+int cioa_meta_write(cioa_chunk *ch, const char *buf, size_t size)    /* cio_meta.c:46-73 */
+{
+    if (!ch || size > 65535) {
+        return -1;
+    }
+    if (!cioa_chunk_is_up(ch)) {
+        return -1;
+    }
+    ch->error_n = 0;
+    unsigned char *meta = ch->map + CIOA_HDR_MIN;
+    const size_t meta_av = cioa_st_meta_len(ch->map);
+    if (meta_av >= size) {                                 /* cio_file.c:1098-1109 */
+        unsigned char *cur_content = ch->map + CIOA_HDR_MIN + meta_av;
+        memcpy(meta, buf, size);
+        memmove(meta + size, cur_content, ch->data_size);
+        return adjust_layout(ch, size);
+    }
+    if (ch->alloc_size < CIOA_HDR_MIN + size + ch->data_size) {
+        if (file_resize(ch, CIOA_HDR_MIN + size + ch->data_size) != CIO_OK) {
+            return -1;
+        }
+    }
+    meta = ch->map + CIOA_HDR_MIN;
+    memmove(meta + size, ch->map + CIOA_HDR_MIN + meta_av, ch->data_size);
+    memcpy(meta, buf, size);
+    return adjust_layout(ch, size);
+}
+
+int cioa_meta_read(cioa_chunk *ch, char **meta_buf, int *meta_len)
+{
+    if (!ch || !ch->map) {
+        return -1;
+    }
+    const int len = cioa_st_meta_len(ch->map);
+    if (len <= 0) {
+        return -1;
+    }
+    *meta_buf = (char *) ch->map + CIOA_HDR_MIN;
+    *meta_len = len;
+    return 0;
+}
+
+int cioa_meta_cmp(cioa_chunk *ch, const char *meta_buf, int meta_len)
+{
+    if (!ch || !ch->map) {
+        return -1;
+    }
+    const int len = cioa_st_meta_len(ch->map);
+    if (len != meta_len) {
+        return -1;
+    }
+    return memcmp(ch->map + CIOA_HDR_MIN, meta_buf, (size_t) meta_len) == 0 ? 0 : -1;
+}
+
+int cioa_meta_size(cioa_chunk *ch)
+{
+    if (!ch || !ch->map) {
+        return -1;
+    }
+    return cioa_st_meta_len(ch->map);
+}
+
+/* ---- sync -------------------------------------------------------------------- */
+
+/* Steps of cio_file_sync (cio_file.c:1147-1250) before the CRC: returns 1 if
+ * the chunk needs a sync, 0 if not, -1 on error. */
+static int sync_prepare(cioa_chunk *ch, size_t *file_size)
+{
+    if (ch->flags & CIO_OPEN_RD) {
+        return 0;
+    }
+    if (!ch->map) {
+        return 0;
+    }
+    if (ch->synced) {
+        return 0;
+    }
+    if (native_get_size(ch, file_size) != CIO_OK) {
+        return -1;
+    }
+    if (ch->ctx->flags & CIO_TRIM_FILES) {                  /* :1192-1224 */
+        size_t desired;
+        const size_t av = ch->alloc_size - CIOA_HDR_MIN - cioa_st_meta_len(ch->map) - ch->data_size;
+        if (av > 0) {
+            desired = ch->alloc_size - av;
+        }
+        else if (ch->alloc_size > *file_size) {
+            desired = ch->alloc_size;
+        }
+        else {
+            desired = *file_size;
+        }
+        if (desired != *file_size) {
+            desired = ROUND_UP(desired, (size_t) ch->ctx->page);
+            if (file_resize(ch, desired) != CIO_OK) {
+                return -1;
+            }
+        }
+    }
+    return 1;
+}
+
+static int sync_commit(cioa_chunk *ch)
+{
+    const int mode = (ch->ctx->flags & CIO_FULL_SYNC) ? MS_SYNC : MS_ASYNC;
+    if (msync(ch->map, ch->alloc_size, mode) != 0) {
+        return -1;
+    }
+    ch->synced = 1;
+    return update_size(ch) == CIO_OK ? 0 : -1;
+}
+
+int cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n)
+{
+    int rc = CIO_OK;
+    size_t m = 0;
+    cio_sync_item *items = NULL;
+    cioa_chunk **bat = NULL;
+    if (n == 0) {
+        return CIO_OK;
+    }
+    items = calloc(n, sizeof(*items));
+    bat = calloc(n, sizeof(*bat));
+    if (!items || !bat) {
+        free(items);
+        free(bat);
+        return CIO_ERROR;
+    }
+    cioa_ctx *ctx = NULL;
+    for (size_t i = 0; i < n; i++) {
+        cioa_chunk *ch = chunks[i];
+        size_t file_size;
+        if (!ch) {
+            continue;
+        }
+        ch->error_n = 0;
+        const int need = sync_prepare(ch, &file_size);
+        if (need < 0) {
+            rc = CIO_ERROR;
+            continue;
+        }
+        if (need == 0) {
+            continue;
+        }
+        if (deferred(ch)) {
+            if (ch->crc_reset) {
+                if (full_recompute(ch) != CIO_OK) {
+                    rc = CIO_ERROR;
+                    continue;
+                }
+                ch->crc_reset = 0;
+            }
+            cio_sync_item *it = &items[m];
+            it->map = ch->map;
+            it->fs_size = ch->alloc_size;
+            it->crc_end = ch->crc_end;
+            it->crc_cur = ch->crc_cur;
+            it->data_end = region_end(ch);
+            bat[m++] = ch;
+            ctx = ch->ctx;
+            continue;
+        }
+        if (ch->ctx->flags & CIO_CHECKSUM) {               /* finalize_checksum (:116-124) */
+            crc_t crc = htonl((uint32_t) crc_finalize((crc_t) ch->crc_cur));
+            memcpy(ch->map + 2, &crc, sizeof(crc));
+        }
+        if (sync_commit(ch) != 0) {
+            rc = CIO_ERROR;
+        }
+    }
+    if (m > 0) {
+        /* one GPU pass for every deferred chunk: CRC of [crc_end, end) seeded
+         * with crc_cur, finalized header written; msync below */
+        if (cio_file_sync_batch_multi(items, m, CIOA_SYNC_FINALIZE, ctx->devs, ctx->ndev) != CIO_OK) {
+            rc = CIO_ERROR;
+        }
+        else {
+            for (size_t k = 0; k < m; k++) {
+                cioa_chunk *ch = bat[k];
+                if (items[k].status != CIO_OK) {
+                    error_set(ch, CIO_ERR_BAD_LAYOUT);
+                    rc = CIO_ERROR;
+                    continue;
+                }
+                ch->crc_cur = items[k].crc_cur;
+                ch->crc_end = items[k].crc_end;
+                if (sync_commit(ch) != 0) {
+                    rc = CIO_ERROR;
+                }
+            }
+        }
+    }
+    free(items);
+    free(bat);
+    return rc;
+}
+
+int cioa_chunk_sync(cioa_chunk *ch)
+{
+    if (!ch) {
+        return -1;
+    }
+    return cioa_chunk_sync_batch(&ch, 1) == CIO_OK ? 0 : -1;
+}
+
+/* ---- content access -------------------------------------------------------- */
+
+int cioa_chunk_get_content(cioa_chunk *ch, char **buf, size_t *size)
+{
+    if (!ch || !ch->map) {
+        return CIO_ERROR;
+    }
+    *size = ch->data_size;
+    *buf = (char *) ch->map + CIOA_HDR_MIN + cioa_st_meta_len(ch->map);
+    return CIO_OK;
+}
+
+int cioa_chunk_get_content_copy(cioa_chunk *ch, void **out_buf, size_t *out_size)   /* cio_file.c:510-558 */
+{
+    int set_down = 0;
+    if (!ch) {
+        return CIO_ERROR;
+    }
+    if (!cioa_chunk_is_up(ch)) {
+        if (cioa_chunk_up_force(ch) != CIO_OK) {
+            return CIO_ERROR;
+        }
+        set_down = 1;
+    }
+    const size_t size = ch->data_size;
+    char *buf = malloc(size + 1);
+    if (!buf) {
+        if (set_down) {
+            cioa_chunk_down(ch);
+        }
+        return CIO_ERROR;
+    }
+    memcpy(buf, ch->map + CIOA_HDR_MIN + cioa_st_meta_len(ch->map), size);
+    buf[size] = '\0';
+    *out_buf = buf;
+    *out_size = size;
+    if (set_down) {
+        cioa_chunk_down(ch);
+    }
+    return CIO_OK;
+}
+
+ssize_t cioa_chunk_get_content_size(cioa_chunk *ch)
+{
+    return ch ? (ssize_t) ch->data_size : -1;
+}
+
+ssize_t cioa_chunk_get_real_size(cioa_chunk *ch)
+{
+    if (!ch) {
+        return -1;
+    }
+    if (ch->fs_size == 0) {
+        size_t s = 0;
+        return native_get_size(ch, &s) == CIO_OK ? (ssize_t) s : 0;
+    }
+    return (ssize_t) ch->fs_size;
+}
+
+char *cioa_chunk_hash(cioa_chunk *ch)
+{
+    return (ch && ch->map) ? (char *) ch->map + 2 : NULL;
+}
+
+unsigned char *cioa_chunk_map(cioa_chunk *ch, size_t *alloc_size)
+{
+    if (alloc_size) {
+        *alloc_size = (ch && ch->map) ? ch->alloc_size : 0;
+    }
+    return ch ? ch->map : NULL;
+}
+
+const char *cioa_chunk_name(cioa_chunk *ch)
+{
+    return ch ? ch->name : NULL;
+}
+
+int cioa_error_get(cioa_chunk *ch)
+{
+    return ch ? ch->error_n : 0;
+}
+
+uint32_t cioa_chunk_crc_cur(cioa_chunk *ch)
+{
+    return ch ? ch->crc_cur : 0;
+}
+
+void cioa_chunk_set_crc_cur(cioa_chunk *ch, uint32_t crc)
+{
+    if (ch) {
+        ch->crc_cur = crc;
+    }
+}
+
+/* ---- lock / transactions (cio_chunk.c:384-502) ------------------------------ */
+
+int cioa_chunk_lock(cioa_chunk *ch)
+{
+    ch->error_n = 0;
+    if (ch->lock) {
+        return CIO_ERROR;
+    }
+    ch->lock = 1;
+    if (cioa_chunk_is_up(ch)) {
+        return cioa_chunk_sync(ch);
+    }
+    return CIO_OK;
+}
+
+int cioa_chunk_unlock(cioa_chunk *ch)
+{
+    ch->error_n = 0;
+    if (!ch->lock) {
+        return CIO_ERROR;
+    }
+    ch->lock = 0;
+    return CIO_OK;
+}
+
+int cioa_chunk_is_locked(cioa_chunk *ch)
+{
+    return ch->lock;
+}
+
+int cioa_chunk_tx_begin(cioa_chunk *ch)
+{
+    ch->error_n = 0;
+    if (cioa_chunk_is_locked(ch)) {
+        return CIO_RETRY;
+    }
+    if (ch->tx_active) {
+        return CIO_OK;
+    }
+    /* the snapshot must be the CRC of everything written so far */
+    if (catch_up(ch) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    ch->tx_active = 1;
+    ch->tx_crc = ch->crc_cur;
+    ch->tx_content_length = ch->data_size;
+    return CIO_OK;
+}
+
+int cioa_chunk_tx_commit(cioa_chunk *ch)
+{
+    ch->error_n = 0;
+    if (cioa_chunk_sync(ch) == -1) {
+        return CIO_ERROR;
+    }
+    ch->tx_active = 0;
+    return CIO_OK;
+}
+
+int cioa_chunk_tx_rollback(cioa_chunk *ch)
+{
+    ch->error_n = 0;
+    if (!ch->tx_active) {
+        return -1;
+    }
+    ch->crc_cur = ch->tx_crc;
+    ch->data_size = ch->tx_content_length;
+    if (deferred(ch) && ch->map) {
+        /* tx_crc covers [22, 24 + meta_len + tx_content_length) of the
+         * current layout, as the reference's restored crc_cur does */
+        ch->crc_end = region_end(ch);
+        ch->crc_reset = 0;
+    }
+    ch->tx_active = 0;
+    return CIO_OK;
+}
+
+/* ---- up / down (cio_file.c:816-959) ----------------------------------------- */
+
+static int file_up(cioa_chunk *ch, int enforced)
+{
+    ch->error_n = 0;
+    if (ch->map) {
+        return CIO_ERROR;
+    }
+    if (native_is_open(ch)) {
+        return CIO_ERROR;
+    }
+    if (enforced && ch->ctx->total_up >= ch->ctx->max_up) {
+        return CIO_ERROR;
+    }
+    if (native_open(ch) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    if (update_size(ch) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    const int ret = mmap_file(ch, ch->fs_size);
+    if (ret == CIO_CORRUPTED || ret == CIO_RETRY) {
+        native_close(ch);
+    }
+    return ret;
+}
+
+int cioa_chunk_up(cioa_chunk *ch)
+{
+    return file_up(ch, 1);
+}
+
+int cioa_chunk_up_force(cioa_chunk *ch)
+{
+    return file_up(ch, 0);
+}
+
+int cioa_chunk_down(cioa_chunk *ch)
+{
+    ch->error_n = 0;
+    if (!ch->map) {
+        return -1;
+    }
+    if (munmap_file(ch) != 0) {
+        return -1;
+    }
+    ch->alloc_size = 0;
+    update_size(ch);
+    native_close(ch);
+    return 0;
+}
+
+/* ---- batched verify-on-load of a stream directory ----------------------- */
+
+struct scan_ent {
+    char *name;
+    cioa_chunk *ch;
+    int prepared;
+};
+
+static int scan_cmp(const void *a, const void *b)
+{
+    return strcmp(((const struct scan_ent *) a)->name, ((const struct scan_ent *) b)->name);
+}
+
+cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext)
+{
+    char dpath[4096];
+    if (!ctx || !stream) {
+        return NULL;
+    }
+    cioa_stream *st = cioa_stream_get(ctx, stream);
+    if (!st && !(st = cioa_stream_create(ctx, stream))) {
+        return NULL;
+    }
+    snprintf(dpath, sizeof(dpath), "%s/%s", ctx->root, stream);
+    DIR *dir = opendir(dpath);
+    if (!dir) {
+        return NULL;
+    }
+    size_t cap = 256, n = 0;
+    struct scan_ent *ents = malloc(cap * sizeof(*ents));
+    const size_t ext_len = ext ? strlen(ext) : 0;
+    struct dirent *de;
+    while (ents && (de = readdir(dir)) != NULL) {
+        if (de->d_name[0] == '.' || de->d_type != DT_REG) {
+            continue;
+        }
+        const size_t len = strlen(de->d_name);
+        if (ext && (len <= ext_len || strncmp(de->d_name + len - ext_len, ext, ext_len) != 0)) {
+            continue;
+        }
+        if (n == cap) {
+            cap *= 2;
+            struct scan_ent *e2 = realloc(ents, cap * sizeof(*ents));
+            if (!e2) {
+                break;
+            }
+            ents = e2;
+        }
+        ents[n].name = strdup(de->d_name);
+        ents[n].ch = NULL;
+        ents[n].prepared = 0;
+        n++;
+    }
+    closedir(dir);
+    if (!ents) {
+        return NULL;
+    }
+    /* readdir order is filesystem-specific; name order makes the budget of
+     * max_chunks_up deterministic */
+    qsort(ents, n, sizeof(*ents), scan_cmp);
+
+    cio_verify_item *items = calloc(n ? n : 1, sizeof(*items));
+    size_t *vidx = calloc(n ? n : 1, sizeof(*vidx));
+    size_t m = 0, budget = ctx->max_up > ctx->total_up ? ctx->max_up - ctx->total_up : 0;
+    int vflags = 0;
+    for (size_t i = 0; i < n && items && vidx; i++) {
+        cioa_chunk *ch = chunk_new(ctx, st, ents[i].name, ctx->flags);
+        if (!ch) {
+            continue;
+        }
+        ents[i].ch = ch;
+        if (budget == 0) {                                   /* registered down */
+            update_size(ch);
+            continue;
+        }
+        int fresh = 0, ret = native_open(ch);
+        if (ret == CIO_OK && update_size(ch) != CIO_OK) {
+            ret = CIO_ERROR;
+        }
+        if (ret == CIO_OK) {
+            ret = map_prepare(ch, ch->fs_size, &fresh);
+        }
+        if (ret != CIO_OK) {
+            ents[i].prepared = ret;                         /* failed before the CRC */
+            continue;
+        }
+        budget--;
+        if (fresh) {
+            ctx->total_up++;
+            ents[i].prepared = 2;
+            continue;
+        }
+        items[m].map = ch->map;
+        items[m].fs_size = ch->fs_size;
+        items[m].taint = 0;
+        vidx[m++] = i;
+        vflags = verify_flags(ch);
+        ents[i].prepared = 1;
+    }
+    int vrc = CIO_OK;
+    if (m > 0) {
+        vrc = cio_file_verify_batch_multi(items, m, vflags, ctx->devs, ctx->ndev);
+    }
+    for (size_t k = 0; k < m; k++) {
+        struct scan_ent *e = &ents[vidx[k]];
+        if (vrc != CIO_OK) {
+            native_unmap(e->ch);
+            e->prepared = CIO_ERROR;
+            continue;
+        }
+        e->prepared = map_finish(e->ch, &items[k]) == CIO_OK ? 2 : CIO_CORRUPTED;
+    }
+    for (size_t i = 0; i < n; i++) {
+        struct scan_ent *e = &ents[i];
+        cioa_chunk *ch = e->ch;
+        if (ch && (e->prepared == 0 || e->prepared == 2)) {
+            chunk_link(ch);
+        }
+        else if (ch) {
+            /* cio_chunk_open failed: not registered; DELETE_IRRECOVERABLE
+             * (cio_scan.c:107-118) */
+            const int err = ch->error_n;
+            native_unmap(ch);
+            native_close(ch);
+            if ((ctx->flags & CIO_DELETE_IRRECOVERABLE) && e->prepared == CIO_CORRUPTED &&
+                (err == CIO_ERR_BAD_CHECKSUM || err == CIO_ERR_BAD_FILE_SIZE || err == CIO_ERR_BAD_LAYOUT)) {
+                (void) unlink(ch->path);
+            }
+            chunk_free(ch);
+        }
+        free(e->name);
+    }
+    free(ents);
+    free(items);
+    free(vidx);
+    return st;
+}
+
+/* ---- benchmark driver (tools/cio.c:367-466) ------------------------------- */
+
+int cioa_bench_perf_write(const char *root, const void *data, size_t len, int files, int writes,
+                          int batch, int flags, double *secs, uint64_t *bytes)
+{
+    char name[64];
+    struct timespec t1, t2;
+    cioa_ctx *ctx = cioa_create(root, flags);
+    if (!ctx) {
+        return CIO_ERROR;
+    }
+    if (batch < 1) {
+        batch = 1;
+    }
+    cioa_set_max_chunks_up(ctx, batch + CIOA_MAX_CHUNKS_UP);
+    cioa_stream *st = cioa_stream_create(ctx, "test-perf");
+    cioa_chunk **group = calloc((size_t) batch, sizeof(*group));
+    if (!st || !group) {
+        free(group);
+        cioa_destroy(ctx);
+        return CIO_ERROR;
+    }
+    const int defer = (flags & CIOA_DEFERRED_CRC) && (flags & CIO_CHECKSUM);
+    uint64_t nb = 0;
+    int rc = CIO_OK, ng = 0, err;
+    clock_gettime(CLOCK_REALTIME, &t1);
+    for (int i = 0; i < files && rc == CIO_OK; i++) {
+        snprintf(name, sizeof(name), "perf-test-%04i.txt", i);
+        cioa_chunk *ch = cioa_chunk_open(ctx, st, name, CIO_OPEN, len, &err);
+        if (!ch) {
+            continue;
+        }
+        for (int j = 0; j < writes; j++) {
+            if (cioa_chunk_write(ch, data, len) != 0) {
+                rc = CIO_ERROR;
+                break;
+            }
+            nb += len;
+        }
+        if (!defer) {
+            cioa_chunk_sync(ch);
+            cioa_chunk_close(ch, 0);
+            continue;
+        }
+        group[ng++] = ch;
+        if (ng == batch || i == files - 1) {
+            if (cioa_chunk_sync_batch(group, (size_t) ng) != CIO_OK) {
+                rc = CIO_ERROR;
+            }
+            for (int k = 0; k < ng; k++) {
+                cioa_chunk_close(group[k], 0);
+            }
+            ng = 0;
+        }
+    }
+    for (int k = 0; k < ng; k++) {
+        cioa_chunk_close(group[k], 0);
+    }
+    clock_gettime(CLOCK_REALTIME, &t2);
+    free(group);
+    cioa_destroy(ctx);
+    if (secs) {
+        *secs = (double) (t2.tv_sec - t1.tv_sec) + (double) (t2.tv_nsec - t1.tv_nsec) * 1e-9;
+    }
+    if (bytes) {
+        *bytes = nb;
+    }
+    return rc;
+}

@@ -37,7 +37,9 @@
 #include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <vector>
 #include <string>
 #include <algorithm>
@@ -1175,18 +1177,25 @@ struct DeviceState {
     uint32_t *xinv8 = nullptr;   // [kStep]: x^(-8 d) (d bytes un-shifted)
 };
 
+// One DeviceState per HIP device, allocated once and never moved: plans and
+// in-flight host batches keep a pointer to it (a growing vector
+// here reallocated under them when a second device was first used).
+constexpr int kMaxDev = 64;
 std::mutex g_mu;
-std::vector<DeviceState> g_dev;
+std::unique_ptr<DeviceState> g_dev[kMaxDev];
 
 int device_state(DeviceState **out)
 {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    std::lock_guard<std::mutex> lk(g_mu);
-    if ((int) g_dev.size() <= dev) {
-        g_dev.resize(dev + 1);
+    if (dev < 0 || dev >= kMaxDev) {
+        return fail("device ordinal out of range");
     }
-    DeviceState &st = g_dev[dev];
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_dev[dev]) {
+        g_dev[dev].reset(new DeviceState());
+    }
+    DeviceState &st = *g_dev[dev];
     if (!st.ready) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
@@ -1883,7 +1892,6 @@ struct PipeSlot {
 };
 
 struct HostPipe {
-    std::mutex mu;
     bool ready = false;
     CopyPool *pool = nullptr;
     PipeSlot slot[kSlots];
@@ -1891,25 +1899,56 @@ struct HostPipe {
     size_t state_cap = 0;
 };
 
-std::mutex g_pipe_mu;
-std::vector<HostPipe *> g_pipes;
+// Pipelines are pooled per device: a call takes an idle one (or builds one,
+// up to CIO_GPU_PIPES_PER_DEV, default 4) and gives it back when done, so
+// concurrent callers on one device, and callers on different devices, run
+// in parallel.  Nothing global is held while a batch runs.
+struct DevPipes {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<HostPipe *> idle;
+    int count = 0;
+};
+DevPipes g_pipes[kMaxDev];
 
-hipError_t pipe_get(HostPipe **out)
+int pipes_per_dev()
 {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) {
-        return e;
+    static const int v = [] {
+        int k = 4;
+        if (const char *r = getenv("CIO_GPU_PIPES_PER_DEV")) {
+            const int x = atoi(r);
+            if (x >= 1 && x <= 64) {
+                k = x;
+            }
+        }
+        return k;
+    }();
+    return v;
+}
+
+hipError_t pipe_acquire(int dev, HostPipe **out)
+{
+    DevPipes &dp = g_pipes[dev];
+    std::unique_lock<std::mutex> lk(dp.mu);
+    dp.cv.wait(lk, [&] { return !dp.idle.empty() || dp.count < pipes_per_dev(); });
+    if (!dp.idle.empty()) {
+        *out = dp.idle.back();
+        dp.idle.pop_back();
+        return hipSuccess;
     }
-    std::lock_guard<std::mutex> lk(g_pipe_mu);
-    if ((int) g_pipes.size() <= dev) {
-        g_pipes.resize(dev + 1, nullptr);
-    }
-    if (!g_pipes[dev]) {
-        g_pipes[dev] = new HostPipe();
-    }
-    *out = g_pipes[dev];
+    dp.count++;
+    *out = new HostPipe();
     return hipSuccess;
+}
+
+void pipe_release(int dev, HostPipe *hp)
+{
+    DevPipes &dp = g_pipes[dev];
+    {
+        std::lock_guard<std::mutex> lk(dp.mu);
+        dp.idle.push_back(hp);
+    }
+    dp.cv.notify_one();
 }
 
 hipError_t pipe_init(HostPipe &hp)
@@ -2015,8 +2054,10 @@ hipError_t stage_plan(PipeSlot &s, const HostGroup &g, DeviceState *st, cio_crc3
 
 // Host ranges pinned in place by cio_crc32_host_register (long-lived chunk
 // mappings).  A group whose every source lies inside one of them skips the
-// staging copy: the DMA engine reads the caller's pages directly.
-std::mutex g_reg_mu;
+// staging copy: the DMA engine reads the caller's pages directly.  Batches
+// hold the registry shared for their whole run (so a range cannot be
+// unregistered under queued DMAs); register/unregister take it exclusively.
+std::shared_mutex g_reg_mu;
 std::vector<std::pair<uintptr_t, size_t>> g_reg;   // (start, length)
 
 bool in_registered(const uint8_t *p, uint64_t len)
@@ -2070,60 +2111,16 @@ hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
     return hipSuccess;
 }
 
-}  // namespace
-
-extern "C" int cio_crc32_host_register(const void *p, size_t len)
+// The single-device host batch on the calling thread's current device.
+int batch_host_current(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
+                       uint32_t *out_raw, size_t n)
 {
-    if (!p || len == 0) {
-        return fail("cio_crc32_host_register: empty range");
-    }
     DeviceState *st;
     if (device_state(&st) != CIO_OK) {
         return CIO_ERROR;
     }
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    for (const auto &r : g_reg) {
-        if (r.first == reinterpret_cast<uintptr_t>(p)) {
-            return fail("cio_crc32_host_register: already registered");
-        }
-    }
-    const hipError_t e = hipHostRegister(const_cast<void *>(p), len, hipHostRegisterDefault);
-    if (e != hipSuccess) {
-        return fail("cio_crc32_host_register", e);
-    }
-    g_reg.emplace_back(reinterpret_cast<uintptr_t>(p), len);
-    return CIO_OK;
-}
-
-extern "C" int cio_crc32_host_unregister(const void *p)
-{
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    for (size_t i = 0; i < g_reg.size(); i++) {
-        if (g_reg[i].first == reinterpret_cast<uintptr_t>(p)) {
-            const hipError_t e = hipHostUnregister(const_cast<void *>(p));
-            g_reg.erase(g_reg.begin() + (long) i);
-            return e == hipSuccess ? CIO_OK : fail("cio_crc32_host_unregister", e);
-        }
-    }
-    return fail("cio_crc32_host_unregister: not registered");
-}
-
-extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
-                                    uint32_t *out_raw, size_t n)
-{
-    if (n == 0) {
-        return CIO_OK;
-    }
-    if (!bufs || !lens || !out_raw) {
-        return fail("cio_crc32_batch_host: null argument");
-    }
-    if (n >= 0xffffffffull) {
-        return fail("cio_crc32_batch_host: too many chunks");
-    }
-    DeviceState *st;
-    if (device_state(&st) != CIO_OK) {
-        return CIO_ERROR;
-    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     // Groups of <= kStage bytes, 16-byte aligned segment placement.
     std::vector<HostGroup> groups(1);
     for (size_t i = 0; i < n; i++) {
@@ -2149,11 +2146,15 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
     }
 
     HostPipe *hp = nullptr;
-    hipError_t e = pipe_get(&hp);
+    hipError_t e = pipe_acquire(dev, &hp);
     if (e != hipSuccess) {
         return fail("cio_crc32_batch_host: device", e);
     }
-    std::lock_guard<std::mutex> lk(hp->mu);
+    struct Release {
+        int dev;
+        HostPipe *hp;
+        ~Release() { pipe_release(dev, hp); }
+    } release{dev, hp};
     if (!hp->ready && (e = pipe_init(*hp)) != hipSuccess) {
         return fail("cio_crc32_batch_host: pipeline setup", e);
     }
@@ -2170,10 +2171,7 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
     if (e == hipSuccess) {
         e = hipStreamSynchronize(s0.stream);
     }
-    // Registered (pinned-in-place) sources: decided per group, under the
-    // registry lock for the whole call so a range cannot be unregistered
-    // while its DMAs are queued.
-    std::lock_guard<std::mutex> rlk(g_reg_mu);
+    std::shared_lock<std::shared_mutex> rlk(g_reg_mu);
     int rc = CIO_OK;
     hipEvent_t prev = nullptr;
     for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
@@ -2225,4 +2223,175 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
         return fail("cio_crc32_batch_host", e);
     }
     return rc;
+}
+
+// Runs fn with `dev` as the calling thread's current device and restores the
+// previous one afterwards.
+template <typename F>
+int on_device(int dev, F fn)
+{
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) {
+        HIP_TRY(hipSetDevice(dev), "hipSetDevice");
+    }
+    const int rc = fn();
+    if (prev != dev) {
+        (void) hipSetDevice(prev);
+    }
+    return rc;
+}
+
+}  // namespace
+
+extern "C" int cio_crc32_host_register(const void *p, size_t len)
+{
+    if (!p || len == 0) {
+        return fail("cio_crc32_host_register: empty range");
+    }
+    DeviceState *st;
+    if (device_state(&st) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    std::unique_lock<std::shared_mutex> lk(g_reg_mu);
+    for (const auto &r : g_reg) {
+        if (r.first == reinterpret_cast<uintptr_t>(p)) {
+            return fail("cio_crc32_host_register: already registered");
+        }
+    }
+    // Portable: the pinned range is DMA-able by every device of the process,
+    // so multi-device batches take the direct path for it too.
+    const hipError_t e = hipHostRegister(const_cast<void *>(p), len, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        return fail("cio_crc32_host_register", e);
+    }
+    g_reg.emplace_back(reinterpret_cast<uintptr_t>(p), len);
+    return CIO_OK;
+}
+
+extern "C" int cio_crc32_host_unregister(const void *p)
+{
+    std::unique_lock<std::shared_mutex> lk(g_reg_mu);
+    for (size_t i = 0; i < g_reg.size(); i++) {
+        if (g_reg[i].first == reinterpret_cast<uintptr_t>(p)) {
+            const hipError_t e = hipHostUnregister(const_cast<void *>(p));
+            g_reg.erase(g_reg.begin() + (long) i);
+            return e == hipSuccess ? CIO_OK : fail("cio_crc32_host_unregister", e);
+        }
+    }
+    return fail("cio_crc32_host_unregister: not registered");
+}
+
+extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
+                                    uint32_t *out_raw, size_t n)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (!bufs || !lens || !out_raw) {
+        return fail("cio_crc32_batch_host: null argument");
+    }
+    if (n >= 0xffffffffull) {
+        return fail("cio_crc32_batch_host: too many chunks");
+    }
+    return batch_host_current(bufs, lens, seeds, out_raw, n);
+}
+
+extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
+                                          uint32_t *out_raw, size_t n, const int *devices, int ndev)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (!bufs || !lens || !out_raw || (ndev > 0 && !devices)) {
+        return fail("cio_crc32_batch_host_multi: null argument");
+    }
+    if (n >= 0xffffffffull) {
+        return fail("cio_crc32_batch_host_multi: too many chunks");
+    }
+    if (ndev <= 0) {
+        return batch_host_current(bufs, lens, seeds, out_raw, n);
+    }
+    int visible = 0;
+    HIP_TRY(hipGetDeviceCount(&visible), "hipGetDeviceCount");
+    for (int d = 0; d < ndev; d++) {
+        if (devices[d] < 0 || devices[d] >= visible || devices[d] >= kMaxDev) {
+            return fail("cio_crc32_batch_host_multi: device ordinal out of range");
+        }
+    }
+    const int G = (int) std::min<size_t>((size_t) ndev, n);
+    if (G == 1) {
+        return on_device(devices[0], [&] { return batch_host_current(bufs, lens, seeds, out_raw, n); });
+    }
+    // Chunk i -> devices[i % G]: one host thread per device entry, each with
+    // its own pipeline, stream and device buffers; no collective, results are
+    // scattered back by chunk index.
+    std::vector<int> rcs(G, CIO_OK);
+    std::vector<std::string> errs(G);
+    std::vector<std::thread> th;
+    th.reserve(G);
+    for (int d = 0; d < G; d++) {
+        th.emplace_back([&, d]() {
+            std::vector<const void *> b;
+            std::vector<size_t> l;
+            std::vector<uint32_t> sd, o;
+            for (size_t i = (size_t) d; i < n; i += (size_t) G) {
+                b.push_back(bufs[i]);
+                l.push_back(lens[i]);
+                if (seeds) {
+                    sd.push_back(seeds[i]);
+                }
+            }
+            o.resize(b.size());
+            if (hipSetDevice(devices[d]) != hipSuccess) {
+                rcs[d] = CIO_ERROR;
+                errs[d] = "hipSetDevice";
+                return;
+            }
+            rcs[d] = batch_host_current(b.data(), l.data(), seeds ? sd.data() : nullptr, o.data(), b.size());
+            if (rcs[d] != CIO_OK) {
+                errs[d] = g_err;
+                return;
+            }
+            size_t k = 0;
+            for (size_t i = (size_t) d; i < n; i += (size_t) G) {
+                out_raw[i] = o[k++];
+            }
+        });
+    }
+    for (auto &t : th) {
+        t.join();
+    }
+    for (int d = 0; d < G; d++) {
+        if (rcs[d] != CIO_OK) {
+            char msg[64];
+            snprintf(msg, sizeof(msg), "cio_crc32_batch_host_multi: device %d", devices[d]);
+            return cioa_fail_msg(msg, errs[d].c_str());
+        }
+    }
+    return CIO_OK;
+}
+
+extern "C" int cio_gpu_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        return 0;
+    }
+    return n;
+}
+
+extern "C" int cio_gpu_set_device(int dev)
+{
+    HIP_TRY(hipSetDevice(dev), "hipSetDevice");
+    return CIO_OK;
+}
+
+extern "C" int cio_gpu_get_device(void)
+{
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        return -1;
+    }
+    return dev;
 }

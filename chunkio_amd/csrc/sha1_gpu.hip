@@ -1,7 +1,7 @@
 // sha1_gpu.hip -- batched SHA-1 content hash over independent chunks (gfx950).
 //
 // Reference path (fluent/chunkio): cio_sha1_init/update/final and
-// cio_sha1_hash (src/cio_sha1.c:91-122) wrap an un-vendored <sha1/sha1.h>
+// cio_sha1_hash (src/cio_sha1.c:26-57) wrap an un-vendored <sha1/sha1.h>
 // whose SHA_CTX / SHA1_Init / SHA1_Update / SHA1_Final API is OpenSSL's
 // (include/chunkio/cio_sha1.h:52).  The algorithm is FIPS 180-4 SHA-1; the
 // digest is the 20-byte big-endian output of SHA1_Final.

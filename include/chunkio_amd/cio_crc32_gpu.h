@@ -27,7 +27,7 @@
  *                                    CRCs into a running cf->crc_cur
  *                                    (src/cio_file.c:97-113)
  *   cio_sha1_batch_dev()             cio_sha1_init/update/final over each chunk
- *                                    (src/cio_sha1.c:91-122)
+ *                                    (src/cio_sha1.c:26-57)
  *
  * CRC values in and out are RAW states (not finalized), exactly what
  * crc_update() takes and returns: seed 0xffffffff (= crc_init()) gives the
@@ -54,6 +54,14 @@ extern "C" {
  * safe).  Called implicitly by every GPU entry point. */
 int cio_gpu_init(void);
 
+/* Devices.  Every single-device entry point runs on the calling thread's
+ * current HIP device; these select it without HIP headers (a chunkio process
+ * drives G GPUs with one host thread per device, or through the *_multi
+ * entry points below).  count: visible devices (0 if none). */
+int cio_gpu_device_count(void);
+int cio_gpu_set_device(int dev);
+int cio_gpu_get_device(void);            /* -1 on error */
+
 /* Human-readable reason for the last CIO_ERROR on this thread ("" if none). */
 const char *cio_gpu_last_error(void);
 
@@ -75,8 +83,9 @@ uint32_t cio_crc32_combine(uint32_t raw_a, uint32_t raw0_b, uint64_t len_b);
 /*
  * A plan fixes the geometry of a batch (n chunks at byte offsets offs[i]
  * with lengths lens[i] from one device base pointer) and uploads the work
- * partition once; executing it is two kernel launches on `stream` with no
- * host synchronisation, so it can be captured in a HIP graph.
+ * partition once, on the calling thread's current device; executing it is ONE
+ * kernel launch on `stream` with no host synchronisation, so it can be
+ * captured in a HIP graph.
  * offs/lens are HOST arrays.  Offsets and lengths may be arbitrary (any byte
  * alignment, zero-length chunks allowed).
  */
@@ -121,15 +130,26 @@ int  cio_crc32_batch_dev(const void *dev_base, const uint64_t *offs,
 int  cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
                           const uint32_t *seeds, uint32_t *out_raw, size_t n);
 
+/* The same batch spread over several GPUs: chunk i goes to
+ * devices[i % ndev], one host thread + pipeline + stream per device entry, no
+ * collective; results are scattered back by index.  A device may be listed
+ * more than once (each entry gets its own pipeline).  ndev <= 0: the current
+ * device, as cio_crc32_batch_host.  Concurrent calls are safe: pipelines are
+ * pooled per device and nothing global is held while a batch runs. */
+int  cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens,
+                                const uint32_t *seeds, uint32_t *out_raw, size_t n,
+                                const int *devices, int ndev);
+
 /* Pin a long-lived host range in place (e.g. a chunk file's MAP_SHARED
  * mapping, cio_file_unix.c:100) so that cio_crc32_batch_host DMAs the chunks
  * inside it directly, skipping the copy into pinned staging.  A staging group
  * takes the direct path only when every one of its chunks lies inside a
  * registered range; others are staged as before, so results never depend on
  * registration.  Registration pins pages (costly: do it once per mapping,
- * not per batch).  CIO_ERROR when the driver cannot pin the range or it is
+ * not per batch).  The range is pinned portable, so every device's pipeline
+ * can DMA it.  CIO_ERROR when the driver cannot pin the range or it is
  * already registered; cio_crc32_host_unregister(p) takes the start address
- * given to register and must not race a batch call using the range. */
+ * given to register and waits for batch calls in flight. */
 int  cio_crc32_host_register(const void *p, size_t len);
 int  cio_crc32_host_unregister(const void *p);
 

@@ -34,6 +34,8 @@ extern "C" {
 
 #define CIOA_SYNC_FINALIZE  1   /* write the finalized CRC (cio_file_sync) */
 #define CIOA_SYNC_MSYNC     2   /* msync(MS_ASYNC) each map after the header write (cio_file.c:1232) */
+#define CIOA_SYNC_FULL      8   /* msync(MS_SYNC) instead: chunkio's CIO_FULL_SYNC (chunkio.h:45,
+                                   cio_file_unix.c:481-486); same value as that flag */
 
 typedef struct cio_sync_item {
     unsigned char *map;   /* writable mapped chunk file: magic C1 00, meta_len (BE u16 @22),
@@ -41,13 +43,24 @@ typedef struct cio_sync_item {
     size_t fs_size;       /* mapped size */
     uint64_t crc_end;     /* in/out: file offset up to which crc_cur is current (>= 22) */
     uint32_t crc_cur;     /* in/out: raw CRC state over [22, crc_end) (cf->crc_cur) */
-    int status;           /* out: CIO_OK, or CIO_CORRUPTED for a bad header / range */
+    int status;           /* out: CIO_OK, CIO_CORRUPTED for a bad header / range, or CIO_ERROR
+                             when msync failed (header written, chunk not durable: the
+                             caller keeps it unsynced, as cio_file_sync does on that error) */
+    uint64_t data_end;    /* in: end of the CRC region, 24 + meta_len + cf->data_size, or 0 to
+                             take it from the header's content length.  They differ after a
+                             transaction rollback (src/cio_chunk.c:476-502 restores data_size
+                             but not the header field) */
 } cio_sync_item;
 
 /* Bring n chunks' CRCs up to date in one GPU batch and write their headers.
  * Returns CIO_OK if the batch ran (items may still be CIO_CORRUPTED),
  * CIO_ERROR on a GPU/library failure (then no header was written). */
 int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags);
+
+/* The same with the CRC pass spread over GPUs (cio_crc32_batch_host_multi:
+ * chunk k -> devices[k % ndev]); ndev <= 0: the current device. */
+int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags,
+                              const int *devices, int ndev);
 
 #ifdef __cplusplus
 }

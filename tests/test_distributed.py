@@ -123,3 +123,18 @@ def test_bench_rank_reductions_gloo_world2():
         assert p.exitcode == 0
     assert got == [10.0, 11.0]
     assert mx == 1.0
+
+
+def test_bench_gpus_n_spawns_ranks_or_refuses(tmp_path):
+    """`python bench.py --gpus N` with no launcher environment starts N rank
+    processes itself (bench.spawn_ranks) and refuses, non-zero, when fewer
+    than N GPUs are visible -- here, on a CPU host, with none visible."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2, r.stderr
+    assert "--gpus 2 but only 0 GPU(s) visible" in r.stderr
+    assert r.stdout == ""

@@ -295,7 +295,7 @@ def test_host_pipeline_reuse_and_growth(cuda):
 
 @pytest.mark.gpu
 def test_host_pipeline_concurrent_callers(cuda):
-    """Two host threads share the per-device pipeline (serialised by its lock)."""
+    """Four host threads on one device: each takes its own pooled pipeline."""
     import threading
     rng = np.random.default_rng(12)
     jobs = [[rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(1, 400000, 300)]
@@ -369,3 +369,85 @@ def test_cfg2_tiled_400kb_full_size(cuda, data400):
     lens = np.full(n, d.size, dtype=np.uint64)
     got = gpu_crc(cuda, np.tile(d, n), offs, lens)
     assert np.all((got ^ np.uint32(0xFFFFFFFF)) == np.uint32(0x777A8F30))
+
+
+@pytest.mark.gpu
+def test_host_batch_multi_device_logical(cuda):
+    """cio_crc32_batch_host_multi with G logical devices mapped onto the
+    box's GPU(s): chunk i -> devices[i % G], one host thread + pipeline per
+    entry, results scattered back by index; equal to the oracle and to the
+    single-device call for G = 1, 2, 3, 5 (more entries than chunks too)."""
+    rng = np.random.default_rng(21)
+    bufs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(0, 600000, 257)]
+    bufs += [np.zeros(0, np.uint8), rng.integers(0, 256, 70 << 20, dtype=np.uint8)]   # spans groups
+    seeds = rng.integers(0, 2 ** 32, len(bufs), dtype=np.uint64).astype(np.uint32)
+    want = [po.crc_update(int(s), b) for s, b in zip(seeds, bufs)]
+    ndev = max(1, cio.device_count())
+    for g in (1, 2, 3, 5):
+        devs = [k % ndev for k in range(g)]
+        got = cio.crc32_batch_host(bufs, seeds=seeds, devices=devs)
+        assert list(map(int, got)) == want, g
+    few = cio.crc32_batch_host(bufs[:2], devices=[0] * 4)
+    assert list(map(int, few)) == [po.crc_update(INIT, b) for b in bufs[:2]]
+    with pytest.raises(cio.CioGpuError):
+        cio.crc32_batch_host(bufs[:2], devices=[ndev + 7])
+
+
+@pytest.mark.gpu
+def test_plan_survives_other_device_init(cuda):
+    """the per-device tables a plan points to must not move
+    when another device is first used.  Create a plan on device 0, initialise
+    every other visible device, then re-execute the plan."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(22)
+    lens = rng.integers(0, 300000, 64).astype(np.uint64)
+    host, offs = wl.host_batch(7, lens, align=16)
+    base = torch.from_numpy(host).to(cuda)
+    plan = cio.Crc32Plan(offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=cuda)
+    plan.exec(base, out)
+    torch.cuda.synchronize()
+    first = out.cpu().numpy().view(np.uint32).copy()
+    lib = cio.lib()
+    for d in range(1, cio.device_count()):
+        assert lib.cio_gpu_set_device(d) == 0 and lib.cio_gpu_init() == 0
+    assert lib.cio_gpu_set_device(0) == 0
+    plan.exec(base, out)
+    torch.cuda.synchronize()
+    again = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(first, again)
+    assert list(map(int, first)) == [po.crc_update(INIT, host[int(o):int(o + n)]) for o, n in zip(offs, lens)]
+    plan.close()
+    del ctypes
+
+
+@pytest.mark.gpu
+def test_verify_paths_multi_device_and_delete(cuda, tmp_path, data400):
+    """cio_verify_paths_multi over logical devices: same verdicts as one
+    device; CIO_DELETE_IRRECOVERABLE removes exactly the corrupted files."""
+    from chunkio_amd import chunkfile as cf
+    paths = []
+    for i in range(40):
+        p = str(tmp_path / "s" / f"c{i:02d}")
+        c, _ = cf.ChunkFile.open(p, deferred_crc=True)
+        c.write(data400[: 10000 * (i + 1)])
+        c.close()
+        paths.append(p)
+    bad = {3: 24 + 77, 17: 3, 31: 0}          # content byte, CRC byte, magic
+    for i, off in bad.items():
+        raw = bytearray(open(paths[i], "rb").read())
+        raw[off] ^= 0x11
+        open(paths[i], "wb").write(bytes(raw))
+    st1, er1, cr1 = cf.verify_paths(paths)
+    ndev = max(1, cio.device_count())
+    st2, er2, cr2 = cf.verify_paths(paths, devices=[k % ndev for k in range(3)])
+    assert np.array_equal(st1, st2) and np.array_equal(er1, er2) and np.array_equal(cr1, cr2)
+    assert [i for i in range(40) if st1[i] != cf.CIO_OK] == sorted(bad)
+    assert [int(er1[i]) for i in sorted(bad)] == [cf.CIO_ERR_BAD_CHECKSUM, cf.CIO_ERR_BAD_CHECKSUM,
+                                                 cf.CIO_ERR_BAD_LAYOUT]
+    st3, _, _ = cf.verify_paths(paths, flags=cf.CIO_CHECKSUM | cf.CIOA_VERIFY_DELETE_IRRECOVERABLE,
+                                devices=[0, 0])
+    assert np.array_equal(st3, st1)
+    import os
+    assert [i for i in range(40) if not os.path.exists(paths[i])] == sorted(bad)
