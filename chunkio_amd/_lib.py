@@ -20,7 +20,7 @@ EXPORTS = (
     "cio_crc32_shift", "cio_crc32_combine",
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_batch_dev", "cio_crc32_batch_host",
-    "cio_crc32_batch_host_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device",
+    "cio_crc32_batch_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device",
     "cio_crc32_host_register", "cio_crc32_host_unregister",
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_gpu_read_stream",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",

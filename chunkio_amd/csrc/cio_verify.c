@@ -12,8 +12,11 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <stdio.h>
+#include <time.h>
 #include <unistd.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -133,71 +136,133 @@ int cio_file_verify_batch(cio_verify_item *items, size_t n, int flags)
     return cio_file_verify_batch_multi(items, n, flags, NULL, 0);
 }
 
-/* ---- open / map / unmap of many files on host threads ------------------ */
+/* ---- verify straight from files ------------------------------------------ *
+ *
+ * cio_verify_paths does not map the files: the header checks pread() the 24
+ * header bytes (and, for the legacy inference, the first content byte), and
+ * the CRC regions go to the GPU pipeline as file ranges that its copy
+ * threads pread() into pinned staging (cio_crc32_batch_fd_multi).  The bytes
+ * checked are the ones a map would show; what is saved is building and
+ * tearing down a page table per file (an munmap of a faulted-in 2 MB map
+ * costs a TLB shootdown across every CPU the process ran on). */
 
 struct path_job {
     const char *const *paths;
-    cio_verify_item *items;
     int *fds;
+    int *status, *error;
+    uint32_t *crc_raw;
+    uint64_t *len;             /* CRC region length (0: not checked) */
+    unsigned char (*hdr)[8];   /* stored header bytes 2..9 */
     size_t lo, hi;
     int flags;
     long page;
 };
 
-static int want_populate(void)
+static double now_s(void)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *r = getenv("CIO_VERIFY_POPULATE");
-        v = r ? atoi(r) != 0 : 1;
-    }
-    return v;
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double) t.tv_sec + (double) t.tv_nsec * 1e-9;
 }
 
-/* cio_file_native_open + get_size + map (cio_file_unix.c:396-417, 317-341,
- * 74-111) for one slice of the paths.  Maps are pre-faulted (MAP_POPULATE)
- * on these threads, so the GPU pipeline's copy threads do not take a page
- * fault per 4 KiB. */
-static void *open_slice(void *arg)
+static int pread_full(int fd, void *buf, size_t n, off_t off)
+{
+    size_t done = 0;
+    while (done < n) {
+        const ssize_t r = pread(fd, (char *) buf + done, n - done, off + (off_t) done);
+        if (r < 0 && errno == EINTR) {
+            continue;
+        }
+        if (r <= 0) {
+            return -1;
+        }
+        done += (size_t) r;
+    }
+    return 0;
+}
+
+/* cio_file_native_open + get_size (cio_file_unix.c:396-417, 317-341), then
+ * mmap_file's and cio_file_format_check's non-CRC steps in the reference's
+ * order (cio_file.c:383-405, 445-464, 202-264) on the file's bytes. */
+static void *check_slice(void *arg)
 {
     struct path_job *j = arg;
     const int rw = (j->flags & CIOA_VERIFY_WRITEBACK) != 0;
-    const int populate = want_populate() ? MAP_POPULATE : 0;
+    const int ck = (j->flags & CIOA_VERIFY_CHECKSUM) != 0;
     for (size_t i = j->lo; i < j->hi; i++) {
         struct stat sb;
-        cio_verify_item *it = &j->items[i];
-        it->map = NULL;
-        it->fs_size = 0;
-        it->status = CIO_OK;
+        unsigned char h[CIOA_HDR_MIN];
+        j->status[i] = CIO_OK;
+        j->error[i] = 0;
+        j->crc_raw[i] = 0;
+        j->len[i] = 0;
         j->fds[i] = open(j->paths[i], rw ? O_RDWR : O_RDONLY);
         if (j->fds[i] < 0 || fstat(j->fds[i], &sb) != 0) {
-            it->status = CIO_ERROR;
+            j->status[i] = CIO_ERROR;
             continue;
         }
-        it->fs_size = (size_t) sb.st_size;
-        if (sb.st_size > 0) {
-            void *p = mmap(NULL, (size_t) sb.st_size, rw ? PROT_READ | PROT_WRITE : PROT_READ,
-                           MAP_SHARED | populate, j->fds[i], 0);
-            if (p == MAP_FAILED) {
-                it->status = CIO_ERROR;
+        const size_t size = (size_t) sb.st_size;
+        if (size == 0) {
+            /* empty: only a read-write open prepares it (init header, crc_cur
+             * = crc_update(init, "\0\0")) */
+            if (!rw) {
+                j->status[i] = CIO_CORRUPTED;
+                j->error[i] = CIO_ERR_PERMISSION;
+                continue;
             }
-            else {
-                it->map = (unsigned char *) p;
+            cioa_write_init_header(h, ck);
+            if (posix_fallocate(j->fds[i], 0, j->page) != 0 ||
+                pwrite(j->fds[i], h, CIOA_HDR_MIN, 0) != CIOA_HDR_MIN) {
+                j->status[i] = CIO_ERROR;
+                continue;
+            }
+            j->crc_raw[i] = ck ? CIOA_CRC_EMPTY_RAW : 0;
+            continue;
+        }
+        if (size < CIOA_HDR_MIN) {
+            j->status[i] = CIO_CORRUPTED;
+            j->error[i] = CIO_ERR_BAD_FILE_SIZE;
+            continue;
+        }
+        if (pread_full(j->fds[i], h, CIOA_HDR_MIN, 0) != 0) {
+            j->status[i] = CIO_ERROR;
+            continue;
+        }
+        const uint16_t meta = cioa_st_meta_len(h);
+        int64_t clen = cioa_st_get_content_len_field(h);
+        const size_t content_offset = CIOA_HDR_MIN + (size_t) meta;
+        if (clen == 0 && size > content_offset) {          /* legacy inference (:166-176) */
+            unsigned char first = 0;
+            if (pread_full(j->fds[i], &first, 1, (off_t) content_offset) != 0) {
+                j->status[i] = CIO_ERROR;
+                continue;
+            }
+            if (first != 0) {
+                clen = (int64_t) size - CIOA_HDR_MIN - meta;
+                if (rw) {
+                    unsigned char be[4];
+                    cioa_st_set_content_len(h, (uint32_t) clen);
+                    memcpy(be, h + CIOA_HDR_CONTENT_LEN_OFF, 4);
+                    if (pwrite(j->fds[i], be, 4, CIOA_HDR_CONTENT_LEN_OFF) != 4) {
+                        j->status[i] = CIO_ERROR;
+                        continue;
+                    }
+                }
             }
         }
-        else if (rw) {
-            /* mmap_file, empty file opened RW: room for the header, one page
-             * (cio_file.c:398-405), then map it for the init header. */
-            void *p = MAP_FAILED;
-            if (posix_fallocate(j->fds[i], 0, j->page) == 0) {
-                p = mmap(NULL, (size_t) j->page, PROT_READ | PROT_WRITE, MAP_SHARED, j->fds[i], 0);
-            }
-            if (p == MAP_FAILED) {
-                it->status = CIO_ERROR;
-            }
-            else {
-                it->map = (unsigned char *) p;
-            }
+        if (h[0] != CIOA_HDR_ID_00 || h[1] != CIOA_HDR_ID_01) {
+            j->status[i] = CIO_CORRUPTED;
+            j->error[i] = CIO_ERR_BAD_LAYOUT;
+            continue;
+        }
+        if ((uint64_t) CIOA_HDR_MIN + meta + (uint64_t) clen > size) {
+            j->status[i] = CIO_CORRUPTED;
+            j->error[i] = CIO_ERR_BAD_FILE_SIZE;
+            continue;
+        }
+        if (ck) {
+            j->len[i] = 2 + (uint64_t) meta + (uint64_t) clen;
+            memcpy(j->hdr[i], h + 2, 8);
         }
     }
     return NULL;
@@ -207,27 +272,22 @@ static void *close_slice(void *arg)
 {
     struct path_job *j = arg;
     for (size_t i = j->lo; i < j->hi; i++) {
-        cio_verify_item *it = &j->items[i];
-        if (it->map) {
-            munmap(it->map, it->fs_size ? it->fs_size : (size_t) j->page);
-        }
         if (j->fds[i] >= 0) {
             close(j->fds[i]);
         }
         /* cio_scan_stream_files with CIO_DELETE_IRRECOVERABLE
          * (src/cio_scan.c:107-118): a chunk that failed its load as
          * CIO_CORRUPTED with a bad checksum, size or layout is deleted. */
-        if ((j->flags & CIOA_VERIFY_DELETE_IRRECOVERABLE) && it->status == CIO_CORRUPTED &&
-            (it->error == CIO_ERR_BAD_CHECKSUM || it->error == CIO_ERR_BAD_FILE_SIZE ||
-             it->error == CIO_ERR_BAD_LAYOUT)) {
+        if ((j->flags & CIOA_VERIFY_DELETE_IRRECOVERABLE) && j->status[i] == CIO_CORRUPTED &&
+            (j->error[i] == CIO_ERR_BAD_CHECKSUM || j->error[i] == CIO_ERR_BAD_FILE_SIZE ||
+             j->error[i] == CIO_ERR_BAD_LAYOUT)) {
             (void) unlink(j->paths[i]);
         }
     }
     return NULL;
 }
 
-static void run_sliced(void *(*fn)(void *), const char *const *paths, cio_verify_item *items, int *fds,
-                       size_t n, int flags)
+static void run_sliced(void *(*fn)(void *), struct path_job proto, size_t n)
 {
     enum { MAX_T = 16 };
     struct path_job jobs[MAX_T];
@@ -237,9 +297,10 @@ static void run_sliced(void *(*fn)(void *), const char *const *paths, cio_verify
     if (T > MAX_T) {
         T = MAX_T;
     }
-    const long page = sysconf(_SC_PAGESIZE);
     for (size_t t = 0; t < T; t++) {
-        jobs[t] = (struct path_job) {paths, items, fds, n * t / T, n * (t + 1) / T, flags, page};
+        jobs[t] = proto;
+        jobs[t].lo = n * t / T;
+        jobs[t].hi = n * (t + 1) / T;
     }
     for (size_t t = 1; t < T; t++) {
         started[t] = pthread_create(&th[t], NULL, fn, &jobs[t]) == 0;
@@ -258,56 +319,89 @@ static void run_sliced(void *(*fn)(void *), const char *const *paths, cio_verify
 int cio_verify_paths_multi(const char *const *paths, size_t n, int flags, const int *devices, int ndev,
                            int *status, int *error, uint32_t *crc_raw)
 {
-    cio_verify_item *items;
-    int *fds;
-    uint8_t *failed;
-    int rc;
-
+    int rc = CIO_OK;
     if (n == 0) {
         return CIO_OK;
     }
     if (!paths) {
         return CIO_ERROR;
     }
-    items = calloc(n, sizeof(*items));
-    fds = malloc(n * sizeof(*fds));
-    failed = calloc(n, 1);
-    if (!items || !fds || !failed) {
-        free(items);
-        free(fds);
-        free(failed);
-        return CIO_ERROR;
+    int *fds = malloc(n * sizeof(int));
+    int *st = malloc(n * sizeof(int));
+    int *er = malloc(n * sizeof(int));
+    uint32_t *cr = malloc(n * sizeof(uint32_t));
+    uint64_t *len = malloc(n * sizeof(uint64_t));
+    unsigned char (*hdr)[8] = malloc(n * 8);
+    int *bfd = malloc(n * sizeof(int));
+    uint64_t *boff = malloc(n * sizeof(uint64_t));
+    size_t *blen = malloc(n * sizeof(size_t));
+    size_t *bidx = malloc(n * sizeof(size_t));
+    uint32_t *raw = malloc(n * sizeof(uint32_t));
+    if (!fds || !st || !er || !cr || !len || !hdr || !bfd || !boff || !blen || !bidx || !raw) {
+        rc = CIO_ERROR;
+        goto out;
     }
-    run_sliced(open_slice, paths, items, fds, n, flags);
-    /* an item whose open/stat/map failed stays CIO_ERROR through the batch */
+    const int timing = getenv("CIO_VERIFY_TIMING") != NULL;
+    const double t0 = timing ? now_s() : 0;
+    struct path_job proto = {paths, fds, st, er, cr, len, hdr, 0, 0, flags, sysconf(_SC_PAGESIZE)};
+    run_sliced(check_slice, proto, n);
+    const double t1 = timing ? now_s() : 0;
+    size_t m = 0;
     for (size_t i = 0; i < n; i++) {
-        failed[i] = items[i].status == CIO_ERROR;
-    }
-    rc = cio_file_verify_batch_multi(items, n, flags, devices, ndev);
-    for (size_t i = 0; i < n; i++) {
-        if (failed[i]) {
-            items[i].status = CIO_ERROR;
-            items[i].error = 0;
-            items[i].crc_raw = 0;
+        if (st[i] == CIO_OK && len[i] > 0) {
+            bfd[m] = fds[i];
+            boff[m] = CIOA_HDR_CONTENT_OFFSET;
+            blen[m] = (size_t) len[i];
+            bidx[m++] = i;
         }
+    }
+    if (m > 0 && cio_crc32_batch_fd_multi(bfd, boff, blen, NULL, raw, m, devices, ndev) != CIO_OK) {
+        rc = CIO_ERROR;
+        proto.flags &= ~CIOA_VERIFY_DELETE_IRRECOVERABLE;     /* nothing is known to be irrecoverable */
+    }
+    else {
+        for (size_t k = 0; k < m; k++) {
+            const size_t i = bidx[k];
+            /* crc_check = htonl(crc_finalize(crc)) in an 8-byte crc_t, 8-byte memcmp */
+            crc_t check = htonl((uint32_t) crc_finalize((crc_t) raw[k]));
+            if (memcmp(hdr[i], &check, sizeof(check)) != 0) {
+                st[i] = CIO_CORRUPTED;
+                er[i] = CIO_ERR_BAD_CHECKSUM;
+            }
+            else {
+                cr[i] = raw[k];
+            }
+        }
+    }
+    const double t2 = timing ? now_s() : 0;
+    run_sliced(close_slice, proto, n);
+    if (timing) {
+        fprintf(stderr, "cio_verify_paths: %zu files, open+headers %.2f ms, CRC batch %.2f ms, close %.2f ms\n",
+                n, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (now_s() - t2) * 1e3);
+    }
+    for (size_t i = 0; i < n; i++) {
         if (status) {
-            status[i] = items[i].status;
+            status[i] = st[i];
         }
         if (error) {
-            error[i] = items[i].error;
+            error[i] = er[i];
         }
         if (crc_raw) {
-            crc_raw[i] = items[i].crc_raw;
+            crc_raw[i] = cr[i];
         }
     }
-    if (rc != CIO_OK) {
-        /* the batch did not run: nothing is known to be irrecoverable */
-        flags &= ~CIOA_VERIFY_DELETE_IRRECOVERABLE;
-    }
-    run_sliced(close_slice, paths, items, fds, n, flags);
-    free(failed);
-    free(items);
+out:
     free(fds);
+    free(st);
+    free(er);
+    free(cr);
+    free(len);
+    free(hdr);
+    free(bfd);
+    free(boff);
+    free(blen);
+    free(bidx);
+    free(raw);
     return rc;
 }
 

@@ -10,9 +10,10 @@
  *   reference                          deferred
  *   write: crc_update(crc_cur, buf)    write: copy only
  *          + raw state at map+2
- *   write_at / metadata: recompute     crc_cur = init, crc_end = 22 (recomputed
- *                                      at once where the legacy length inference
- *                                      makes the reference hash more than the data)
+ *   write_at / metadata: recompute     crc_cur = init, crc_end = 22 (recomputed at
+ *                                      once where the reference's recompute would
+ *                                      not hash exactly the data region: a stale
+ *                                      length after a rollback, legacy inference)
  *   sync: finalize crc_cur             sync: crc_update(crc_cur, map[crc_end..end))
  *                                            on the GPU, then finalize (batched
  *                                            over many chunks by sync_batch)
@@ -268,32 +269,29 @@ static int calculate_checksum(cioa_chunk *ch, uint32_t *out)
     return cio_crc32_batch_host_multi(&buf, &len, &seed, out, 1, ch->ctx->devs, ch->ctx->ndev);
 }
 
-/* Would cio_file_calculate_checksum run the legacy length inference now
- * (cio_file_st.h:166-176: untainted chunk, zero length field, non-zero first
- * content byte)?  Then its CRC covers the inferred region, not the data. */
-static int legacy_inference_due(cioa_chunk *ch)
+/* Does cio_file_calculate_checksum (cio_file.c:66-94) hash exactly the data
+ * region [22, 24 + meta_len + data_size) right now?  It takes the length from
+ * the header, so it does not after a transaction rollback (which restores
+ * data_size but not the header field, cio_chunk.c:494-497), nor when the
+ * legacy length inference fires (cio_file_st.h:166-176: untainted chunk,
+ * zero length field, non-zero first content byte). */
+static int recompute_is_data_region(cioa_chunk *ch)
 {
-    if (ch->taint || cioa_st_get_content_len_field(ch->map) != 0) {
-        return 0;
-    }
-    if (ch->fs_size == 0) {
-        update_size(ch);
-    }
-    const size_t content_offset = CIOA_HDR_MIN + (size_t) cioa_st_meta_len(ch->map);
-    return ch->fs_size > content_offset && content_offset < ch->alloc_size && ch->map[content_offset] != 0;
+    const int64_t clen = cioa_st_content_len(ch->map, ch->fs_size, ch->taint, 0);
+    return clen >= 0 && (uint64_t) clen == (uint64_t) ch->data_size;
 }
 
 /* Full recompute (write_at reset, metadata move).  Immediate mode, and the
- * deferred mode when the legacy inference would make the reference hash
- * more than the data: crc_update(init, region) now, on the GPU.  Otherwise
- * (deferred) the recompute folds into the next sync: crc_end = 22. */
+ * deferred mode when the reference would hash something other than the data
+ * region: crc_update(init, region) now, on the GPU.  Otherwise (deferred)
+ * the recompute folds into the next sync: crc_end = 22. */
 static int full_recompute(cioa_chunk *ch)
 {
     ch->crc_cur = 0xffffffffu;
     if (ch->fs_size == 0) {
         update_size(ch);                 /* as cio_file_calculate_checksum does (:73-75) */
     }
-    if (deferred(ch) && !legacy_inference_due(ch)) {
+    if (deferred(ch) && recompute_is_data_region(ch)) {
         ch->crc_end = CIOA_HDR_CONTENT_OFFSET;
         return CIO_OK;
     }
@@ -375,7 +373,7 @@ static int map_prepare(cioa_chunk *ch, size_t size, int *fresh)
             return CIO_ERROR;
         }
     }
-    if (native_map(ch, size, fs_size > 0) != CIO_OK) {
+    if (native_map(ch, size, 0) != CIO_OK) {
         return CIO_ERROR;
     }
     if (fs_size > 0) {

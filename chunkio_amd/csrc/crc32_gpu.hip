@@ -1746,6 +1746,8 @@ int cio_gpu_stream_sync(void *stream)
 
 #include <thread>
 #include <condition_variable>
+#include <errno.h>
+#include <unistd.h>
 
 namespace {
 
@@ -1769,8 +1771,14 @@ static size_t stage_bytes()
 #define kStage (stage_bytes())
 constexpr int kSlots = 3;
 
+// One staging group.  A source is host memory (src[k]) or, for batches read
+// straight from files, a file range (fd[k], foff[k]) that the copy threads
+// pread() into the pinned buffer: no mapping, no page faults, no TLB
+// shootdowns at unmap.
 struct HostGroup {
     std::vector<const uint8_t *> src;
+    std::vector<int> fd;               // empty for memory sources
+    std::vector<uint64_t> foff;
     std::vector<uint64_t> offs, lens;
     std::vector<uint32_t> cid;
     uint64_t bytes = 0;
@@ -1800,12 +1808,12 @@ public:
             w.join();
         }
     }
-    void copy(uint8_t *dst, const HostGroup &g)
+    // false if a file source could not be read in full
+    bool copy(uint8_t *dst, const HostGroup &g)
     {
         const size_t parts = std::min<size_t>(workers_.size() + 1, std::max<size_t>(1, g.bytes >> 22));
         if (parts <= 1) {
-            slice(dst, g, 0, 1);
-            return;
+            return slice(dst, g, 0, 1);
         }
         {
             std::lock_guard<std::mutex> lk(mu_);
@@ -1813,26 +1821,47 @@ public:
             g_ = &g;
             parts_ = parts;
             pending_ = parts - 1;
+            failed_ = false;
             ++gen_;
         }
         cv_.notify_all();
-        slice(dst, g, 0, parts);
+        const bool ok = slice(dst, g, 0, parts);
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [this] { return pending_ == 0; });
+        return ok && !failed_;
     }
 
 private:
-    static void slice(uint8_t *dst, const HostGroup &g, size_t t, size_t parts)
+    static bool slice(uint8_t *dst, const HostGroup &g, size_t t, size_t parts)
     {
         const uint64_t per = (g.bytes + parts - 1) / parts;
         const uint64_t lo = t * per, hi = std::min<uint64_t>(g.bytes, lo + per);
-        for (size_t k = 0; k < g.src.size(); k++) {
+        bool ok = true;
+        for (size_t k = 0; k < g.offs.size(); k++) {
             const uint64_t a = g.offs[k], b = a + g.lens[k];
             const uint64_t x = std::max(a, lo), y = std::min(b, hi);
-            if (x < y) {
+            if (x >= y) {
+                continue;
+            }
+            if (g.fd.empty()) {
                 memcpy(dst + x, g.src[k] + (x - a), y - x);
+                continue;
+            }
+            uint64_t done = 0;
+            while (done < y - x) {
+                const ssize_t r = pread(g.fd[k], dst + x + done, y - x - done,
+                                        (off_t) (g.foff[k] + (x - a) + done));
+                if (r <= 0) {
+                    if (r < 0 && errno == EINTR) {
+                        continue;
+                    }
+                    ok = false;
+                    break;
+                }
+                done += (uint64_t) r;
             }
         }
+        return ok;
     }
     void run(size_t id)
     {
@@ -1853,8 +1882,9 @@ private:
                 parts = parts_;
             }
             if (id < parts) {
-                slice(dst, *g, id, parts);
+                const bool ok = slice(dst, *g, id, parts);
                 std::lock_guard<std::mutex> lk(mu_);
+                failed_ = failed_ || !ok;
                 if (--pending_ == 0) {
                     done_cv_.notify_one();
                 }
@@ -1865,6 +1895,7 @@ private:
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     bool stop_ = false;
+    bool failed_ = false;
     uint64_t gen_ = 0;
     uint8_t *dst_ = nullptr;
     const HostGroup *g_ = nullptr;
@@ -2073,7 +2104,7 @@ bool in_registered(const uint8_t *p, uint64_t len)
 
 bool group_registered(const HostGroup &g)
 {
-    if (g_reg.empty()) {
+    if (g_reg.empty() || !g.fd.empty()) {
         return false;
     }
     for (size_t k = 0; k < g.src.size(); k++) {
@@ -2112,8 +2143,10 @@ hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
 }
 
 // The single-device host batch on the calling thread's current device.
-int batch_host_current(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
-                       uint32_t *out_raw, size_t n)
+// Sources are bufs[i] (host memory), or file ranges (fds[i], foffs[i]) when
+// fds is given.
+int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *foffs, const size_t *lens,
+                       const uint32_t *seeds, uint32_t *out_raw, size_t n)
 {
     DeviceState *st;
     if (device_state(&st) != CIO_OK) {
@@ -2124,7 +2157,7 @@ int batch_host_current(const void *const *bufs, const size_t *lens, const uint32
     // Groups of <= kStage bytes, 16-byte aligned segment placement.
     std::vector<HostGroup> groups(1);
     for (size_t i = 0; i < n; i++) {
-        const uint8_t *p = reinterpret_cast<const uint8_t *>(bufs[i]);
+        const uint8_t *p = fds ? nullptr : reinterpret_cast<const uint8_t *>(bufs[i]);
         uint64_t left = lens[i], done = 0;
         do {
             HostGroup *g = &groups.back();
@@ -2135,7 +2168,11 @@ int batch_host_current(const void *const *bufs, const size_t *lens, const uint32
                 at = 0;
             }
             const uint64_t take = std::min<uint64_t>(left, kStage - at);
-            g->src.push_back(p + done);
+            if (fds) {
+                g->fd.push_back(fds[i]);
+                g->foff.push_back(foffs[i] + done);
+            }
+            g->src.push_back(p ? p + done : nullptr);
             g->offs.push_back(at);
             g->lens.push_back(take);
             g->cid.push_back((uint32_t) i);
@@ -2196,7 +2233,10 @@ int batch_host_current(const void *const *bufs, const size_t *lens, const uint32
         if (direct) {
             if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
         } else {
-            hp->pool->copy(s.pinned, g);
+            if (!hp->pool->copy(s.pinned, g)) {
+                rc = fail("cio_crc32_batch: short read from a file source");
+                break;
+            }
             if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
         }
         if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
@@ -2294,38 +2334,34 @@ extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens,
     if (n >= 0xffffffffull) {
         return fail("cio_crc32_batch_host: too many chunks");
     }
-    return batch_host_current(bufs, lens, seeds, out_raw, n);
+    return batch_host_current(bufs, nullptr, nullptr, lens, seeds, out_raw, n);
 }
 
-extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
-                                          uint32_t *out_raw, size_t n, const int *devices, int ndev)
+namespace {
+
+// Chunk i -> devices[i % G]: one host thread per device entry, each with its
+// own pipeline, stream and device buffers; no collective, results are
+// scattered back by chunk index.
+int batch_multi(const void *const *bufs, const int *fds, const uint64_t *foffs, const size_t *lens,
+                const uint32_t *seeds, uint32_t *out_raw, size_t n, const int *devices, int ndev,
+                const char *what)
 {
-    if (n == 0) {
-        return CIO_OK;
-    }
-    if (!bufs || !lens || !out_raw || (ndev > 0 && !devices)) {
-        return fail("cio_crc32_batch_host_multi: null argument");
-    }
-    if (n >= 0xffffffffull) {
-        return fail("cio_crc32_batch_host_multi: too many chunks");
-    }
     if (ndev <= 0) {
-        return batch_host_current(bufs, lens, seeds, out_raw, n);
+        return batch_host_current(bufs, fds, foffs, lens, seeds, out_raw, n);
     }
     int visible = 0;
     HIP_TRY(hipGetDeviceCount(&visible), "hipGetDeviceCount");
     for (int d = 0; d < ndev; d++) {
         if (devices[d] < 0 || devices[d] >= visible || devices[d] >= kMaxDev) {
-            return fail("cio_crc32_batch_host_multi: device ordinal out of range");
+            return cioa_fail_msg(what, "device ordinal out of range");
         }
     }
     const int G = (int) std::min<size_t>((size_t) ndev, n);
     if (G == 1) {
-        return on_device(devices[0], [&] { return batch_host_current(bufs, lens, seeds, out_raw, n); });
+        return on_device(devices[0], [&] {
+            return batch_host_current(bufs, fds, foffs, lens, seeds, out_raw, n);
+        });
     }
-    // Chunk i -> devices[i % G]: one host thread per device entry, each with
-    // its own pipeline, stream and device buffers; no collective, results are
-    // scattered back by chunk index.
     std::vector<int> rcs(G, CIO_OK);
     std::vector<std::string> errs(G);
     std::vector<std::thread> th;
@@ -2333,22 +2369,31 @@ extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t 
     for (int d = 0; d < G; d++) {
         th.emplace_back([&, d]() {
             std::vector<const void *> b;
+            std::vector<int> f;
+            std::vector<uint64_t> fo;
             std::vector<size_t> l;
             std::vector<uint32_t> sd, o;
             for (size_t i = (size_t) d; i < n; i += (size_t) G) {
-                b.push_back(bufs[i]);
+                if (fds) {
+                    f.push_back(fds[i]);
+                    fo.push_back(foffs[i]);
+                } else {
+                    b.push_back(bufs[i]);
+                }
                 l.push_back(lens[i]);
                 if (seeds) {
                     sd.push_back(seeds[i]);
                 }
             }
-            o.resize(b.size());
+            o.resize(l.size());
             if (hipSetDevice(devices[d]) != hipSuccess) {
                 rcs[d] = CIO_ERROR;
                 errs[d] = "hipSetDevice";
                 return;
             }
-            rcs[d] = batch_host_current(b.data(), l.data(), seeds ? sd.data() : nullptr, o.data(), b.size());
+            rcs[d] = batch_host_current(fds ? nullptr : b.data(), fds ? f.data() : nullptr,
+                                        fds ? fo.data() : nullptr, l.data(), seeds ? sd.data() : nullptr,
+                                        o.data(), l.size());
             if (rcs[d] != CIO_OK) {
                 errs[d] = g_err;
                 return;
@@ -2364,12 +2409,46 @@ extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t 
     }
     for (int d = 0; d < G; d++) {
         if (rcs[d] != CIO_OK) {
-            char msg[64];
-            snprintf(msg, sizeof(msg), "cio_crc32_batch_host_multi: device %d", devices[d]);
+            char msg[96];
+            snprintf(msg, sizeof(msg), "%s: device %d", what, devices[d]);
             return cioa_fail_msg(msg, errs[d].c_str());
         }
     }
     return CIO_OK;
+}
+
+}  // namespace
+
+extern "C" int cio_crc32_batch_fd_multi(const int *fds, const uint64_t *foffs, const size_t *lens,
+                                        const uint32_t *seeds, uint32_t *out_raw, size_t n,
+                                        const int *devices, int ndev)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (!fds || !foffs || !lens || !out_raw || (ndev > 0 && !devices)) {
+        return fail("cio_crc32_batch_fd_multi: null argument");
+    }
+    if (n >= 0xffffffffull) {
+        return fail("cio_crc32_batch_fd_multi: too many chunks");
+    }
+    return batch_multi(nullptr, fds, foffs, lens, seeds, out_raw, n, devices, ndev, "cio_crc32_batch_fd_multi");
+}
+
+extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
+                                          uint32_t *out_raw, size_t n, const int *devices, int ndev)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (!bufs || !lens || !out_raw || (ndev > 0 && !devices)) {
+        return fail("cio_crc32_batch_host_multi: null argument");
+    }
+    if (n >= 0xffffffffull) {
+        return fail("cio_crc32_batch_host_multi: too many chunks");
+    }
+    return batch_multi(bufs, nullptr, nullptr, lens, seeds, out_raw, n, devices, ndev,
+                       "cio_crc32_batch_host_multi");
 }
 
 extern "C" int cio_gpu_device_count(void)

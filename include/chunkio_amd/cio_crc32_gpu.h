@@ -140,6 +140,15 @@ int  cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens,
                                 const uint32_t *seeds, uint32_t *out_raw, size_t n,
                                 const int *devices, int ndev);
 
+/* The same over file ranges: chunk i is bytes [foffs[i], foffs[i] + lens[i])
+ * of the open file fds[i], read by the pipeline's copy threads with pread()
+ * straight into pinned staging (no mapping).  For batch verifies of chunk
+ * files that are not otherwise mapped (cio_verify_paths).  CIO_ERROR if a
+ * range cannot be read in full. */
+int  cio_crc32_batch_fd_multi(const int *fds, const uint64_t *foffs, const size_t *lens,
+                              const uint32_t *seeds, uint32_t *out_raw, size_t n,
+                              const int *devices, int ndev);
+
 /* Pin a long-lived host range in place (e.g. a chunk file's MAP_SHARED
  * mapping, cio_file_unix.c:100) so that cio_crc32_batch_host DMAs the chunks
  * inside it directly, skipping the copy into pinned staging.  A staging group
