@@ -1744,9 +1744,11 @@ int cio_gpu_stream_sync(void *stream)
 // outputs go through a chunk-id map into one running-state array on the
 // device, so a chunk split over several groups chains its state on the GPU.
 
+#include <atomic>
 #include <thread>
 #include <condition_variable>
 #include <errno.h>
+#include <time.h>
 #include <unistd.h>
 
 namespace {
@@ -1785,16 +1787,21 @@ struct HostGroup {
 };
 
 // Persistent host copy workers (the box's CPU share per GPU is 16 threads).
-// copy() splits a group's byte range evenly over the workers and the caller,
-// and returns when every slice is in the pinned buffer.
+// copy() cuts a group's byte range into 1 MiB pieces that the workers and
+// the caller claim through one atomic counter, so a slow or descheduled
+// thread delays the group by one piece, not by a 1/16 slice.  The caller
+// first runs `before` (the group's plan build), overlapping it with the
+// workers' copying.
 class CopyPool {
 public:
+    static constexpr uint64_t kPiece = 1ull << 20;
+
     CopyPool()
     {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned nw = std::min(15u, hw > 1 ? hw - 1 : 0u);
         for (unsigned t = 0; t < nw; t++) {
-            workers_.emplace_back([this, t]() { run(t + 1); });
+            workers_.emplace_back([this]() { run(); });
         }
     }
     ~CopyPool()
@@ -1809,35 +1816,52 @@ public:
         }
     }
     // false if a file source could not be read in full
-    bool copy(uint8_t *dst, const HostGroup &g)
+    template <typename F>
+    bool copy(uint8_t *dst, const HostGroup &g, F before)
     {
-        const size_t parts = std::min<size_t>(workers_.size() + 1, std::max<size_t>(1, g.bytes >> 22));
-        if (parts <= 1) {
-            return slice(dst, g, 0, 1);
+        const uint64_t npieces = (g.bytes + kPiece - 1) / kPiece;
+        if (npieces <= 1 || workers_.empty()) {
+            before();
+            return range(dst, g, 0, g.bytes);
         }
         {
             std::lock_guard<std::mutex> lk(mu_);
             dst_ = dst;
             g_ = &g;
-            parts_ = parts;
-            pending_ = parts - 1;
+            npieces_ = npieces;
+            next_.store(0, std::memory_order_relaxed);
+            pending_ = workers_.size();
             failed_ = false;
             ++gen_;
         }
         cv_.notify_all();
-        const bool ok = slice(dst, g, 0, parts);
+        before();
+        const bool ok = drain(dst, g, npieces);
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [this] { return pending_ == 0; });
         return ok && !failed_;
     }
 
 private:
-    static bool slice(uint8_t *dst, const HostGroup &g, size_t t, size_t parts)
+    bool drain(uint8_t *dst, const HostGroup &g, uint64_t npieces)
     {
-        const uint64_t per = (g.bytes + parts - 1) / parts;
-        const uint64_t lo = t * per, hi = std::min<uint64_t>(g.bytes, lo + per);
         bool ok = true;
-        for (size_t k = 0; k < g.offs.size(); k++) {
+        for (;;) {
+            const uint64_t p = next_.fetch_add(1, std::memory_order_relaxed);
+            if (p >= npieces) {
+                return ok;
+            }
+            ok &= range(dst, g, p * kPiece, std::min<uint64_t>(g.bytes, (p + 1) * kPiece));
+        }
+    }
+    // Bytes [lo, hi) of the group's staging image.
+    static bool range(uint8_t *dst, const HostGroup &g, uint64_t lo, uint64_t hi)
+    {
+        // first chunk ending after lo (offs increase along the group)
+        size_t k = (size_t) (std::upper_bound(g.offs.begin(), g.offs.end(), lo) - g.offs.begin());
+        k = k ? k - 1 : 0;
+        bool ok = true;
+        for (; k < g.offs.size() && g.offs[k] < hi; k++) {
             const uint64_t a = g.offs[k], b = a + g.lens[k];
             const uint64_t x = std::max(a, lo), y = std::min(b, hi);
             if (x >= y) {
@@ -1863,13 +1887,13 @@ private:
         }
         return ok;
     }
-    void run(size_t id)
+    void run()
     {
         uint64_t seen = 0;
         for (;;) {
             uint8_t *dst;
             const HostGroup *g;
-            size_t parts;
+            uint64_t npieces;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
@@ -1879,15 +1903,13 @@ private:
                 seen = gen_;
                 dst = dst_;
                 g = g_;
-                parts = parts_;
+                npieces = npieces_;
             }
-            if (id < parts) {
-                const bool ok = slice(dst, *g, id, parts);
-                std::lock_guard<std::mutex> lk(mu_);
-                failed_ = failed_ || !ok;
-                if (--pending_ == 0) {
-                    done_cv_.notify_one();
-                }
+            const bool ok = drain(dst, *g, npieces);
+            std::lock_guard<std::mutex> lk(mu_);
+            failed_ = failed_ || !ok;
+            if (--pending_ == 0) {
+                done_cv_.notify_one();
             }
         }
     }
@@ -1899,7 +1921,9 @@ private:
     uint64_t gen_ = 0;
     uint8_t *dst_ = nullptr;
     const HostGroup *g_ = nullptr;
-    size_t parts_ = 0, pending_ = 0;
+    uint64_t npieces_ = 0;
+    std::atomic<uint64_t> next_{0};
+    size_t pending_ = 0;
 };
 
 size_t align256(size_t x)
@@ -2142,6 +2166,13 @@ hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
     return hipSuccess;
 }
 
+double wall_s()
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double) t.tv_sec + (double) t.tv_nsec * 1e-9;
+}
+
 // The single-device host batch on the calling thread's current device.
 // Sources are bufs[i] (host memory), or file ranges (fds[i], foffs[i]) when
 // fds is given.
@@ -2211,20 +2242,49 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     std::shared_lock<std::shared_mutex> rlk(g_reg_mu);
     int rc = CIO_OK;
     hipEvent_t prev = nullptr;
+    // CIO_GPU_PIPE_TIMING=1: per-call breakdown on stderr (diagnostic)
+    static const bool timing = getenv("CIO_GPU_PIPE_TIMING") != nullptr;
+    double t_copy = 0, t_wait = 0, t_plan = 0;
+    const double t_start = timing ? wall_s() : 0;
     for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
         PipeSlot &s = hp->slot[gi % kSlots];
         const HostGroup &g = groups[gi];
         const bool direct = group_registered(g);
+        double t = timing ? wall_s() : 0;
         if (s.busy) {
             // The slot's previous group (gi - kSlots) must be fully done.
             if ((e = hipEventSynchronize(s.done)) != hipSuccess) break;
             s.busy = false;
         }
+        if (timing) {
+            t_wait += wall_s() - t;
+        }
         cio_crc32_plan view;
         uint32_t *d_cid = nullptr;
         size_t meta_bytes = 0;
         const char *err = nullptr;
-        if ((e = stage_plan(s, g, st, view, &d_cid, &meta_bytes, &err)) != hipSuccess) break;
+        // the group's plan (host image into the slot's pinned arena)
+        auto build = [&] {
+            const double tp = timing ? wall_s() : 0;
+            e = stage_plan(s, g, st, view, &d_cid, &meta_bytes, &err);
+            if (timing) {
+                t_plan += wall_s() - tp;
+            }
+        };
+        if (direct) {
+            build();
+        } else {
+            // staged: the plan is built while the copy workers fill the slot
+            const double tc = timing ? wall_s() : 0;
+            if (!hp->pool->copy(s.pinned, g, build)) {
+                rc = fail("cio_crc32_batch: short read from a file source");
+                break;
+            }
+            if (timing) {
+                t_copy += wall_s() - tc;
+            }
+        }
+        if (e != hipSuccess) break;
         if (err) {
             rc = fail(err);
             break;
@@ -2233,10 +2293,6 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
         if (direct) {
             if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
         } else {
-            if (!hp->pool->copy(s.pinned, g)) {
-                rc = fail("cio_crc32_batch: short read from a file source");
-                break;
-            }
             if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
         }
         if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
@@ -2258,6 +2314,15 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     }
     if (e == hipSuccess && rc == CIO_OK) {
         e = hipMemcpy(out_raw, hp->state, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    }
+    if (timing) {
+        uint64_t total = 0;
+        for (const auto &g : groups) {
+            total += g.bytes;
+        }
+        fprintf(stderr, "batch_host: dev %d, %zu chunks, %zu groups, %.1f MB: total %.2f ms, copy %.2f ms, "
+                        "slot waits %.2f ms, plans %.2f ms\n", dev, n, groups.size(), total / 1e6,
+                (wall_s() - t_start) * 1e3, t_copy * 1e3, t_wait * 1e3, t_plan * 1e3);
     }
     if (e != hipSuccess) {
         return fail("cio_crc32_batch_host", e);
