@@ -60,7 +60,7 @@ constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
 constexpr uint32_t kShiftOff = kSliceBytes;
 constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
-constexpr int kStampWords = 8;
+constexpr int kStampWords = 12;
               // diagnostic stamps per wave (CIO_GPU_STAMPS)
 
 struct ChunkDesc {
@@ -161,14 +161,40 @@ __device__ __forceinline__ uint32_t fold_full(const uint32_t (&s)[kSub])
     return h;
 }
 
+// floor(x / d) for x < 2^52, d >= 1: a correctly rounded double quotient is
+// within one of the integer quotient (x and d are exact in a double), and one
+// compare-and-step fixes it.  A 64-bit integer division is a ~120-instruction
+// SALU routine for wave-uniform operands; at kernel start 16 waves per CU
+// running three of them on the CU's one scalar unit delayed the last wave's
+// first HBM request by ~2.5 us.  This is ~20 VALU instructions per wave.
+__device__ __forceinline__ uint64_t div_u52(uint64_t x, uint64_t d)
+{
+    uint64_t q = (uint64_t) ((double) x / (double) d);
+    if (q * d > x) {
+        q -= 1;
+    } else if ((q + 1) * d <= x) {
+        q += 1;
+    }
+    return q;
+}
+
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t) v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32));
+    return ((uint64_t) hi << 32) | lo;
+}
+
+// The plan guarantees S < 2^40 and W <= 2^12 (plan_create), so both
+// numerators stay below 2^52.
 __device__ __forceinline__ uint64_t wave_start(uint64_t w, uint64_t S, uint64_t W)
 {
-    return (w * S) / W;
+    return div_u52(w * S, W);
 }
 
 __device__ __forceinline__ uint64_t wave_of_step(uint64_t g, uint64_t S, uint64_t W)
 {
-    return ((g + 1) * W + S - 1) / S - 1;
+    return div_u52((g + 1) * W + S - 1, S) - 1;
 }
 
 // Slice tables in LDS, replicated 32x so lane l always reads bank (l & 31):
@@ -292,51 +318,38 @@ __device__ __forceinline__ void table_entries(uint32_t k, uint32_t b, uint32_t &
     }
 }
 
-// Tables.  Phase 1: thread tid computes entry b = tid & 255 of slice
-// table k = tid >> 8 and of shift table k into compact 4 KiB arrays
-// parked in the shift-table region.  Phase 2: every thread gathers the
-// 10 entries of its granules.  Phase 3: consecutive lanes write
-// consecutive 16-byte granules of the replicated images (bank-conflict
-// free: a thread writing 128 contiguous bytes puts a whole wave on 4 banks).
+// Tables.  Thread tid owns entry b = tid & 255 of slice table k = tid >> 8
+// (and of shift table k): the 1024 threads of the workgroup hold the 4 x 256
+// entries exactly once.  Each replicated row of an entry is contiguous in
+// the LDS images -- 32 replicas = 128 B of the slice image, 8 replicas =
+// 32 B of the shift image -- so the thread writes its own rows directly:
+// 8 + 2 ds_write_b128, no compact staging arrays, no gather, one barrier
+// (by the caller).  Lane l writes granule (l + i) & 7 of its row in store i,
+// so the 8 lanes of a ds_write_b128 lane group hit 8 different granules of
+// their 256 B-strided rows: conflict-free.
 constexpr int kE = 1024 / kThreads;            // table entries per thread
+static_assert(kE == 1, "one slice and one shift entry per thread");
 
+template <bool STAMPS = false>
 __device__ __forceinline__ void write_tables(char *lds, uint32_t tid, const uint32_t (&tab_v)[kE],
-                                             const uint32_t (&tab_sv)[kE])
+                                             const uint32_t (&tab_sv)[kE], unsigned long long *ts = nullptr)
 {
-    uint32_t *cslice = reinterpret_cast<uint32_t *>(lds + kShiftOff);
-    uint32_t *cshift = cslice + 1024;
+    const uint32_t k = tid >> 8, b = tid & 255u, lane = tid & 63u;
+    const uint32_t srow = (k >> 1) * 65536u + b * 256u + (k & 1u) * 128u;
+    const uint4 sv = make_uint4(tab_v[0], tab_v[0], tab_v[0], tab_v[0]);
 #pragma unroll
-    for (int e = 0; e < kE; ++e) {
-        cslice[tid + kThreads * e] = tab_v[e];
-        cshift[tid + kThreads * e] = tab_sv[e];
+    for (int i = 0; i < 8; ++i) {
+        *reinterpret_cast<uint4 *>(lds + srow + 16u * ((lane + (uint32_t) i) & 7u)) = sv;
     }
-    __syncthreads();
-    constexpr int kSG = 8192 / kThreads, kHG = 2048 / kThreads;   // granules per thread
-    uint32_t sv[kSG], hv[kHG];
+    const uint32_t hrow = kShiftOff + k * 8192u + b * 32u;
+    const uint4 hv = make_uint4(tab_sv[0], tab_sv[0], tab_sv[0], tab_sv[0]);
 #pragma unroll
-    for (int i = 0; i < kSG; ++i) {
-        // slice image granule g: byte address 16 g -> table pair g >> 12,
-        // entry b = (g >> 4) & 255, table half (g >> 3) & 1
-        const uint32_t g = tid + (uint32_t) kThreads * i;
-        const uint32_t k = 2u * (g >> 12) + ((g >> 3) & 1u);
-        sv[i] = cslice[(k << 8) | ((g >> 4) & 255u)];
+    for (int i = 0; i < 2; ++i) {
+        *reinterpret_cast<uint4 *>(lds + hrow + 16u * ((lane + (uint32_t) i) & 1u)) = hv;
     }
-#pragma unroll
-    for (int i = 0; i < kHG; ++i) {
-        // shift image granule g: byte address 16 g = k*8192 + b*32 + replica
-        const uint32_t g = tid + (uint32_t) kThreads * i;
-        hv[i] = cshift[((g >> 9) << 8) | ((g >> 1) & 255u)];
-    }
-    __syncthreads();
-    uint4 *img = reinterpret_cast<uint4 *>(lds);
-#pragma unroll
-    for (int i = 0; i < kSG; ++i) {
-        img[tid + (uint32_t) kThreads * i] = make_uint4(sv[i], sv[i], sv[i], sv[i]);
-    }
-    uint4 *simg = reinterpret_cast<uint4 *>(lds + kShiftOff);
-#pragma unroll
-    for (int i = 0; i < kHG; ++i) {
-        simg[tid + (uint32_t) kThreads * i] = make_uint4(hv[i], hv[i], hv[i], hv[i]);
+    if (STAMPS) {
+        ts[0] = __builtin_amdgcn_s_memrealtime();
+        ts[1] = ts[0];
     }
 }
 
@@ -511,7 +524,13 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
     }
 }
 
-template <bool STAMPS = false, int PRIO = 1>
+// UNIFORM: the plan's batch is uniform (equal lengths, constant stride), so
+// a wave's first chunk and its descriptor follow from the kernel arguments
+// alone (all preloaded into SGPRs): the first HBM requests wait on no memory
+// access.  The general path reads its WaveStart record first.  Separate
+// instantiations keep the general path's scalar-load wait out of the
+// uniform one's prologue.
+template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
                     uint32_t W, uint32_t unsteps, uint32_t uh,
@@ -525,18 +544,10 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
-    unsigned long long t_entry = 0, t_tables = 0, t_stream = 0, t_first = 0, t_mid = 0;
+    unsigned long long t_entry = 0, t_tables = 0, t_stream = 0, t_first = 0, t_mid = 0, t_issued = 0;
+    unsigned long long t_wt[2] = {0, 0}, t_step1 = 0;
     if (STAMPS) {
         t_entry = __builtin_amdgcn_s_memrealtime();
-    }
-
-    // Table entries are computed, not loaded: at kernel start every global
-    // load pays cold-cache latency, and the build sits on the critical path.
-    uint32_t tab_v[kE], tab_sv[kE];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-        const uint32_t idx = tid + (uint32_t) kThreads * e;
-        table_entries(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u, tab_v[e], tab_sv[e]);
     }
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
@@ -545,8 +556,8 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     const uint32_t lb_hi = lb_lo | 0x10000u;
     const uint32_t lrep = (lane & 7u) << 2;
     const uint32_t slot_group = __builtin_amdgcn_readfirstlane((tid >> 6) >> 2);
-    const uint64_t g0 = wave_start(wave, S, W);
-    const uint64_t gend = wave_start((uint64_t) wave + 1, S, W);
+    const uint64_t g0 = uniform_u64(wave_start(wave, S, W));
+    const uint64_t gend = uniform_u64(wave_start((uint64_t) wave + 1, S, W));
     const bool active = g0 < gend;
 
     // Compute cursor (c, d, j) and load cursor (lc, ld, lj) walk the same
@@ -556,11 +567,11 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     uint32_t j = 0, lj = 0;    // step within the chunk (nsteps is 32-bit)
     uint64_t nload = 0;
     if (active) {
-        if (unsteps) {
+        if (UNIFORM) {
             // Uniform batch (equal lengths, constant 16-byte-multiple stride):
             // the first chunk and its descriptor follow from the kernel
             // arguments, so the first loads wait on no memory access.
-            c = (uint32_t) (g0 / unsteps);
+            c = __builtin_amdgcn_readfirstlane((uint32_t) div_u52(g0, unsteps));
             d.a = ua0 + (uint64_t) c * ustride;
             d.vlen = uvlen;
             d.g = (uint64_t) c * unsteps;
@@ -580,10 +591,13 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     }
 
     // Waves without steps (only when the batch has fewer steps than waves)
-    // point their loads at the always-valid 4 KiB slice table.
-    const uint8_t *lbase = active ? base : reinterpret_cast<const uint8_t *>(g_slice);
+    // point their loads at bytes that are always readable: the first granule
+    // of chunk 0 in a uniform batch (every chunk there has >= 4 content
+    // bytes), else the 4 KiB slice table.  The uniform choice needs no
+    // kernel-argument load, so nothing in the uniform prologue waits on one.
+    const uint8_t *lbase = (UNIFORM || active) ? base : reinterpret_cast<const uint8_t *>(g_slice);
     if (!active) {
-        ld.a = 0;
+        ld.a = UNIFORM ? ua0 : 0;
         ld.vlen = kGran;
         ld.nsteps = 1;
     }
@@ -596,7 +610,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         if (nload > 0) {
             --nload;
             if (++lj == ld.nsteps && nload > 0) {
-                if (unsteps) {
+                if (UNIFORM) {
                     ++lc;
                     ld.a += ustride;
                     ld.g += unsteps;
@@ -617,6 +631,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // no-load path into the vmcnt state and make the table build wait for the ring.
     StepRegs cur;
     issue(cur);
+    // The data requests leave first; the bookkeeping loads below need
+    // kernel-argument pointers (scalar loads) and must not hold them back.
+    __builtin_amdgcn_sched_barrier(0);
     // Descriptors of the first 64 chunks from c0 (one per lane) for the
     // arrival step at the end; fetched now so that they cost nothing there.
     // Clamped, not predicated: a branch would break the ring's vmcnt tracking.
@@ -634,10 +651,23 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // (fold_full); the lane part x^(8 * 16 (63 - l)) is fetched once here
     // instead of gathered from g_x8 at every piece end.
     const uint32_t xl = g_x8[kRow - (lane + 1) * kGran];
-    // Keep the scheduler from sinking these loads below the table build.
+    // Keep the scheduler from sinking these loads below the table build (and
+    // the table arithmetic from rising above them: the first step's HBM
+    // requests leave before any table work).
     __builtin_amdgcn_sched_barrier(0);
+    if (STAMPS) {
+        t_issued = __builtin_amdgcn_s_memrealtime();
+    }
 
-    write_tables(lds, tid, tab_v, tab_sv);
+    // Table entries are computed, not loaded: at kernel start every global
+    // load pays cold-cache latency, and the build sits on the critical path.
+    uint32_t tab_v[kE], tab_sv[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t idx = tid + (uint32_t) kThreads * e;
+        table_entries(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u, tab_v[e], tab_sv[e]);
+    }
+    write_tables<STAMPS>(lds, tid, tab_v, tab_sv, t_wt);
     __syncthreads();
     if (STAMPS) {
         t_tables = __builtin_amdgcn_s_memrealtime();
@@ -711,7 +741,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     if (g < gend) {
-                        if (unsteps) {
+                        if (UNIFORM) {
                             ++c;
                             d.a += ustride;
                             d.g += unsteps;
@@ -742,15 +772,13 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         }
         const uint64_t iters = gend - g0;
         for (uint64_t it = 0; it < iters; ++it) {
-            if (PRIO == 1) {
+            if (PRIO) {
                 rotate_prio(slot_group, it);
-            } else if (PRIO >= 2) {
-                // Time-sliced: the 4 waves of a SIMD always hold 4 distinct
-                // levels and each holds every level for equal time (slices of
-                // 2^(10 + PRIO) shader clocks), whatever their progress.
-                rotate_prio(slot_group, __builtin_amdgcn_s_memtime() >> (10 + PRIO));
             }
             const bool pe = crc_step(cur);
+            if (STAMPS && it == 0) {
+                t_step1 = __builtin_amdgcn_s_memrealtime();
+            }
             if (nload > 0) {
                 issue(cur);
             }
@@ -820,6 +848,10 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         stamps[kStampWords * wave + 5] = xcc_id;
         stamps[kStampWords * wave + 6] = t_first;
         stamps[kStampWords * wave + 7] = t_mid;
+        stamps[kStampWords * wave + 8] = t_issued;   // first step's loads issued
+        stamps[kStampWords * wave + 9] = t_wt[0];    // table build: compact arrays written
+        stamps[kStampWords * wave + 10] = t_wt[1];   // table build: gathered
+        stamps[kStampWords * wave + 11] = t_step1;  // first step CRC'd
     }
 }
 
@@ -881,27 +913,21 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
 template <bool UNI, bool SEEDS>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t uvlen, uint32_t uh,
-                   uint32_t W, const ChunkDesc *__restrict__ desc, const uint32_t *__restrict__ tiny,
-                   const uint32_t *__restrict__ seeds, uint32_t *out,
-                   const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_xinv8,
-                   uint32_t n, uint32_t ntiny)
+                   uint32_t W, uint32_t n, uint32_t ntiny, const ChunkDesc *__restrict__ desc,
+                   const uint32_t *__restrict__ tiny, const uint32_t *__restrict__ seeds, uint32_t *out,
+                   const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_xinv8)
 {
+    // (n and ntiny come before the pointers: the first eight arguments are
+    // preloaded into SGPRs, so the first requests wait on no argument load.)
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
-    uint32_t tab_v[kE], tab_sv[kE];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-        const uint32_t idx = tid + (uint32_t) kThreads * e;
-        table_entries<cx_xpow8n(kRow - kGran)>(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u,
-                                               tab_v[e], tab_sv[e]);
-    }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
     const uint32_t lane = tid & 63u;
     const uint32_t lb_lo = (lane & 31u) << 2;
     const uint32_t lb_hi = lb_lo | 0x10000u;
     const uint32_t lrep = (lane & 7u) << 2;
-    const uint32_t c0 = (uint32_t) (((uint64_t) wave * n) / W);
-    const uint32_t c1 = (uint32_t) (((uint64_t) (wave + 1) * n) / W);
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t) div_u52((uint64_t) wave * n, W));
+    const uint32_t c1 = __builtin_amdgcn_readfirstlane((uint32_t) div_u52((uint64_t) (wave + 1) * n, W));
     const uint32_t lbyte = lane * kGran;
     // Valid dummy address for the optional seeds (the value is discarded).
     const uint32_t *const seeds_p = seeds ? seeds : g_x8;
@@ -933,7 +959,9 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         bool live;
         geom(cc, a, vlen, h, live);
         const uint32_t last = (max(vlen, 1u) - 1u) & ~15u;
-        const uint8_t *src = in ? base + a : reinterpret_cast<const uint8_t *>(g_x8);
+        // A uniform batch re-reads its first chunk (no kernel-argument load
+        // on the way to the first request); the general one the g_x8 table.
+        const uint8_t *src = in ? base + a : (UNI ? base + ua0 : reinterpret_cast<const uint8_t *>(g_x8));
 #pragma unroll
         for (int q = 0; q < kSub; ++q) {
             r.q[q] = ldg16(src + min(lbyte + (uint32_t) q * kRow, last));
@@ -946,11 +974,6 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         }
     };
 
-    // x^(8 * 16 (63 - l)): the lane's fold factor (requested first: the
-    // register matrix below waits for it).
-    const uint32_t xl = g_x8[kRow - kGran * (lane + 1u)];
-    // Uniform batch: one un-shift factor for every chunk.
-    const uint32_t inv_u = UNI ? g_xinv8[(uint32_t) kStep - min((uint32_t) uvlen, (uint32_t) kStep)] : 0u;
 #if SMALL_SLOTS == 2
     SmallRegs ra, rb;
     issue(ra, c0);
@@ -960,6 +983,20 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     issue(cur, c0);
 #endif
     __builtin_amdgcn_sched_barrier(0);
+    // x^(8 * 16 (63 - l)): the lane's fold factor (the register matrix below
+    // waits for it), requested right behind the first data.
+    const uint32_t xl = g_x8[kRow - kGran * (lane + 1u)];
+    // Uniform batch: one un-shift factor for every chunk.
+    const uint32_t inv_u = UNI ? g_xinv8[(uint32_t) kStep - min((uint32_t) uvlen, (uint32_t) kStep)] : 0u;
+    __builtin_amdgcn_sched_barrier(0);
+    // Table entries after the first requests (see crc32_stream_kernel).
+    uint32_t tab_v[kE], tab_sv[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t idx = tid + (uint32_t) kThreads * e;
+        table_entries<cx_xpow8n(kRow - kGran)>(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u,
+                                               tab_v[e], tab_sv[e]);
+    }
     write_tables(lds, tid, tab_v, tab_sv);
     // The multiply by xl as a 32 x 32 GF(2) matrix held in registers: column
     // j = xl * x^(31 - j) (reflected bit j).
@@ -1246,7 +1283,7 @@ struct cio_crc32_plan {
     uint32_t W = 0;            // waves in the grid
     uint32_t grid = 0;         // workgroups
     uint32_t ntiny = 0;        // chunks with len < 4 (byte-serial)
-    int prio = 1;              // CIO_GPU_PRIO: 0 none, 1 per-step rotation, 2/3 time-sliced rotation
+    int prio = 1;              // CIO_GPU_PRIO: 0 none, 1 per-step rotation (2/3, time-sliced, measured slower and removed)
     uint64_t ustride = 0, ua0 = 0, uvlen = 0;   // uniform batch geometry (unsteps > 0)
     uint32_t unsteps = 0, uh = 0;
     bool small = false;        // every chunk fits one wave-step: crc32_small_kernel
@@ -1305,7 +1342,7 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     p->n = (uint32_t) n;
     if (const char *r = getenv("CIO_GPU_PRIO")) {
         const int v = atoi(r);
-        p->prio = (v >= 0 && v <= 3) ? v : 1;
+        p->prio = (v == 0) ? 0 : 1;
     }
     p->grid = (uint32_t) st->cus;
     p->W = p->grid * (kThreads / kWave);
@@ -1344,6 +1381,11 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
         }
         S += ns;
         bytes += lens[i];
+    }
+    // The kernels' start-up divisions (div_u52) need w * S < 2^52 for w <= W
+    // <= 2^12: 2^40 wave-steps is 4 PiB, far past any device's memory.
+    if (S >= (1ull << 40) || W > 4096) {
+        return "cio_crc32_plan_create: batch too large";
     }
     ph.S = S;
     ph.bytes = bytes;
@@ -1546,19 +1588,19 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 }  // extern "C"
 
-using StreamKernel = decltype(&crc32_stream_kernel<false, 1>);
+using StreamKernel = decltype(&crc32_stream_kernel<false, 1, false>);
 
-static StreamKernel select_kernel(int prio, bool stamps)
+static StreamKernel select_kernel(int prio, bool stamps, bool uniform)
 {
-    switch (prio * 2 + (stamps ? 1 : 0)) {
-    case 0: return crc32_stream_kernel<false, 0>;
-    case 1: return crc32_stream_kernel<true, 0>;
-    case 3: return crc32_stream_kernel<true, 1>;
-    case 4: return crc32_stream_kernel<false, 2>;
-    case 5: return crc32_stream_kernel<true, 2>;
-    case 6: return crc32_stream_kernel<false, 3>;
-    case 7: return crc32_stream_kernel<true, 3>;
-    default: return crc32_stream_kernel<false, 1>;
+    switch ((prio ? 4 : 0) + (stamps ? 2 : 0) + (uniform ? 1 : 0)) {
+    case 0: return crc32_stream_kernel<false, 0, false>;
+    case 1: return crc32_stream_kernel<false, 0, true>;
+    case 2: return crc32_stream_kernel<true, 0, false>;
+    case 3: return crc32_stream_kernel<true, 0, true>;
+    case 4: return crc32_stream_kernel<false, 1, false>;
+    case 5: return crc32_stream_kernel<false, 1, true>;
+    case 6: return crc32_stream_kernel<true, 1, false>;
+    default: return crc32_stream_kernel<true, 1, true>;
     }
 }
 
@@ -1588,14 +1630,14 @@ static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const u
                              : (dev_seeds ? crc32_small_kernel<false, true> : crc32_small_kernel<false, false>);
         hipLaunchKernelGGL(sk, dim3(p->grid), dim3(kThreads), 0, s,
                            reinterpret_cast<const uint8_t *>(dev_base), p->ustride, p->ua0, p->uvlen, p->uh,
-                           p->W, p->desc, p->tiny, dev_seeds, dev_out, st->x8, st->xinv8, p->n, p->ntiny);
+                           p->W, p->n, p->ntiny, p->desc, p->tiny, dev_seeds, dev_out, st->x8, st->xinv8);
         HIP_TRY(hipGetLastError(), "crc32_small_kernel launch");
         if (ev1) {
             HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");
         }
         return CIO_OK;
     }
-    auto kern = select_kernel(p->prio, p->stamps != nullptr);
+    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
                        p->W, p->unsteps, p->uh, p->desc, p->wstart, p->tiny,

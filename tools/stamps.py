@@ -36,10 +36,11 @@ def main():
         for k in range(16):
             plan.exec(bufs[(it + k) % 4], out)
         torch.cuda.synchronize()
-        st = np.zeros(4096 * 8 * 2, np.uint64)
+        st = np.zeros(4096 * 12 * 2, np.uint64)
         W = f(plan._handle, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), st.size)
-        raw = st[:W * 8].reshape(W, 8).astype(np.int64)
-        t = np.concatenate([raw[:, :4], raw[:, 6:8]], axis=1)   # entry, tables, stream, exit, first, mid
+        raw = st[:W * 12].reshape(W, 12).astype(np.int64)
+        # entry, tables, stream, exit, first, mid, loads issued, build phase 1, build phase 2
+        t = np.concatenate([raw[:, :4], raw[:, 6:12]], axis=1)
         hw, xcc = raw[:, 4], raw[:, 5]
         simd = (hw >> 4) & 3
         print("   simd of wave slot (WG 0..3):", [list(simd.reshape(-1, 16)[b]) for b in range(4)])
@@ -49,9 +50,13 @@ def main():
         q = lambda a: " ".join(f"{np.percentile(a, p):7.2f}" for p in (0, 10, 50, 90, 100))  # noqa: E731
         print(f"{cfg} iter {it}: span {us[:, 3].max():7.2f} us   [pct 0/10/50/90/100]")
         print("   entry      ", q(us[:, 0]))
+        print("   loads issued", q(us[:, 6]))
+        print("   build ph1   ", q(us[:, 7]))
+        print("   build ph2   ", q(us[:, 8]))
         print("   tables done", q(us[:, 1]))
         print("   first step ", q(us[:, 4]))
         print("   first-tabl ", q(us[:, 4] - us[:, 1]))
+        print("   step 1 done", q(us[:, 9]))
         print("   mid step   ", q(us[:, 5]))
         print("   1st half   ", q(us[:, 5] - us[:, 4]), " 2nd half", q(us[:, 2] - us[:, 5]))
         print("   stream done", q(us[:, 2]))
