@@ -56,6 +56,12 @@ $(LIB): $(COBJS) $(HOBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# A/B variant of the library: make ablib VAR=name DEFS="-DFOO" -> chunkio_amd/lib/ab/name.so
+ablib:
+	@mkdir -p $(OUT)/ab $(BLD)/ab
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(BLD)/ab/crc32_gpu_$(VAR).o $(SRC)/crc32_gpu.hip
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(OUT)/ab/$(VAR).so $(COBJS) $(BLD)/ab/crc32_gpu_$(VAR).o $(BLD)/sha1_gpu.o -lpthread
+
 asm: $(SRC)/crc32_gpu.hip
 	@mkdir -p $(BLD)/asm
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(BLD)/asm/crc32_gpu.s $<
@@ -64,4 +70,4 @@ clean:
 	rm -rf $(BLD) $(LIB) $(CTEST)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean ctests
+.PHONY: all oracle asm clean ctests ablib

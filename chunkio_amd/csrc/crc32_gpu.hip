@@ -446,13 +446,27 @@ __device__ __forceinline__ uint4 head_fix(uint4 v, uint32_t lane, uint32_t h, ui
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// XOR over the 64 lanes of a wave (every lane active), wave-uniform result.
+// DPP moves inside each 16-lane row (quad swaps, then the half-row and row
+// mirrors) leave every lane holding its row's XOR; four lane reads combine
+// the rows.  Plain VALU: __shfl_xor would be six ds_bpermute round trips
+// through the LDS pipe that the CRC lookups are using.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        v ^= __shfl_xor(v, o);
-    }
-    return v;
+    v ^= (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    v ^= (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    v ^= (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    v ^= (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x140, 0xF, 0xF, false);   // row_mirror
+    return (uint32_t) (__builtin_amdgcn_readlane((int) v, 0) ^ __builtin_amdgcn_readlane((int) v, 16) ^
+                       __builtin_amdgcn_readlane((int) v, 32) ^ __builtin_amdgcn_readlane((int) v, 48));
+}
+
+// x ^ (m & c) as one v_bitop3_b32 (truth table 0x78 over x, m, c).
+__device__ __forceinline__ uint32_t xor_and(uint32_t x, uint32_t m, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(x), "v"(m), "v"(c));
+    return r;
 }
 
 // All pieces of chunk c folded into one raw CRC by the last wave to publish
@@ -514,6 +528,9 @@ __device__ __forceinline__ void tiny_chunks(const char *lds, uint32_t lb_lo, con
 // iterations, every wave of a SIMD holds each priority level once: the
 // hardware's age tie-break otherwise lets the oldest wave of each SIMD run
 // ~30% ahead of the youngest, and the workgroup ends with the youngest.
+#ifndef CIOA_PRIO_TAIL
+#define CIOA_PRIO_TAIL 0
+#endif
 __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 {
     switch ((slot_group + (uint32_t) it) & 3u) {
@@ -773,6 +790,11 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         const uint64_t iters = gend - g0;
         for (uint64_t it = 0; it < iters; ++it) {
             if (PRIO) {
+#if CIOA_PRIO_TAIL
+                if (it + CIOA_PRIO_TAIL >= iters) {
+                    __builtin_amdgcn_s_setprio(3);
+                } else
+#endif
                 rotate_prio(slot_group, it);
             }
             const bool pe = crc_step(cur);
@@ -1050,10 +1072,11 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         if (live) {
             uint32_t x = st;
             if (!(SMALL_EXP & 1)) {
-                x = 0;
+                // 32 x (bit-field sign extend, fused and-xor)
+                x = col[0] & (0u - (st & 1u));
 #pragma unroll
-                for (int j = 0; j < 32; ++j) {
-                    x ^= col[j] & (0u - ((st >> j) & 1u));
+                for (int j = 1; j < 32; ++j) {
+                    x = xor_and(x, 0u - ((st >> j) & 1u), col[j]);
                 }
             }
             uint32_t crc = wave_xor(x);

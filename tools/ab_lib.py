@@ -63,7 +63,8 @@ def main():
     for cfg in args.cfg.split(","):
         lens = {"cfg2": wl.cfg2_lens, "cfg3": wl.cfg3_lens,
                 "big": lambda: np.full(1024, 4 << 20, np.uint64),
-                "small": lambda: np.full(65536, 4096, np.uint64)}[cfg]()
+                "small": lambda: np.full(65536, 4096, np.uint64),
+                "cfg4k": lambda: np.full(102400, 4096, np.uint64)}[cfg]()
         lens = np.ascontiguousarray(lens, dtype=np.uint64)
         offs = np.ascontiguousarray(wl.packed_offsets(lens, align=16), dtype=np.uint64)
         total = int(wl.batch_bytes(offs, lens))
