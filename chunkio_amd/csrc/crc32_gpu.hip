@@ -1028,6 +1028,16 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     for (int j = 30; j >= 0; --j) {
         col[j] = (col[j + 1] >> 1) ^ (CIOA_POLY & (0u - (col[j + 1] & 1u)));
     }
+    // Uniform batch without seeds: the head granule's fix-up (clear the bytes
+    // before the content, XOR the initial 0xffffffff in) is the same for every
+    // chunk, so its per-lane masks are computed once here.
+    uint32_t hk[4] = {~0u, ~0u, ~0u, ~0u}, hs[4] = {0u, 0u, 0u, 0u};
+    if (UNI && !SEEDS) {
+        const uint4 k = head_fix(make_uint4(~0u, ~0u, ~0u, ~0u), lane, uh, 0u);
+        const uint4 x = head_fix(make_uint4(0u, 0u, 0u, 0u), lane, uh, 0xffffffffu);
+        hk[0] = k.x; hk[1] = k.y; hk[2] = k.z; hk[3] = k.w;
+        hs[0] = x.x; hs[1] = x.y; hs[2] = x.z; hs[3] = x.w;
+    }
     __syncthreads();
 
     auto chunk = [&](SmallRegs &cur, uint32_t c) {
@@ -1044,7 +1054,12 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
             for (int q = 0; q < kSub; ++q) {
                 r.q[q] = cur.q[q];
             }
-            r.q[0] = head_fix(r.q[0], lane, h, seed);
+            if (UNI && !SEEDS) {
+                r.q[0] = make_uint4((r.q[0].x & hk[0]) ^ hs[0], (r.q[0].y & hk[1]) ^ hs[1],
+                                    (r.q[0].z & hk[2]) ^ hs[2], (r.q[0].w & hk[3]) ^ hs[3]);
+            } else {
+                r.q[0] = head_fix(r.q[0], lane, h, seed);
+            }
             if (vlen < (uint32_t) kStep) {
 #pragma unroll
                 for (int q = 0; q < kSub; ++q) {
