@@ -528,9 +528,6 @@ __device__ __forceinline__ void tiny_chunks(const char *lds, uint32_t lb_lo, con
 // iterations, every wave of a SIMD holds each priority level once: the
 // hardware's age tie-break otherwise lets the oldest wave of each SIMD run
 // ~30% ahead of the youngest, and the workgroup ends with the youngest.
-#ifndef CIOA_PRIO_TAIL
-#define CIOA_PRIO_TAIL 0
-#endif
 __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 {
     switch ((slot_group + (uint32_t) it) & 3u) {
@@ -790,11 +787,6 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         const uint64_t iters = gend - g0;
         for (uint64_t it = 0; it < iters; ++it) {
             if (PRIO) {
-#if CIOA_PRIO_TAIL
-                if (it + CIOA_PRIO_TAIL >= iters) {
-                    __builtin_amdgcn_s_setprio(3);
-                } else
-#endif
                 rotate_prio(slot_group, it);
             }
             const bool pe = crc_step(cur);
@@ -1137,7 +1129,38 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
             acc ^= __builtin_nontemporal_load(p + q * kWave);
         }
     };
-    if (B == 0) {
+    if (B == 0xffffffffu) {
+        // diagnostic (CIO_GPU_RS_BLOCK=-1): the contiguous split with two
+        // steps in flight per wave (the last two refills re-read the last step)
+        const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
+        if (g0 < g1) {
+            auto ld4 = [&](u32x4 *r, uint64_t g) {
+                const u32x4 *p = reinterpret_cast<const u32x4 *>(base + min(g, g1 - 1) * kStep +
+                                                                 (uint64_t) lane * kGran);
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    r[q] = __builtin_nontemporal_load(p + q * kWave);
+                }
+            };
+            u32x4 ra[kSub], rb[kSub];
+            ld4(ra, g0);
+            ld4(rb, g0 + 1);
+            for (uint64_t g = g0; g < g1; g += 2) {
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    acc ^= ra[q];
+                }
+                ld4(ra, g + 2);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    acc ^= rb[q];
+                }
+                ld4(rb, g + 3);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    } else if (B == 0) {
         // the CRC kernel's split: one contiguous range per wave
         const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
         for (uint64_t g = g0; g < g1; ++g) {
