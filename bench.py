@@ -614,8 +614,8 @@ def run_verify(args, rank, world, device, dist):
     chunk files as `tools/cio -k -p` leaves them (2,068,480 B each: header,
     5 x 400kb.txt, CRC 0x088740E7; one of them with a flipped content byte)
     on the box's /tmp (page cache), verified by ONE cio_verify_paths call
-    (open + mmap + header/length checks + one batched GPU CRC pass + 8-byte
-    compare + munmap).  Beside it, the reference's per-file verify
+    (open + header/length checks + pread of the CRC regions into the GPU
+    pipeline + one batched GPU CRC pass + 8-byte compare + close).  Beside it, the reference's per-file verify
     (cio_file_format_check, src/cio_file.c:266-290: crc_update over
     [22, 24 + meta + content) then compare) with the reference's own
     crc_update (oracle/_ref), single thread, over the same mapped files."""
@@ -685,7 +685,7 @@ def run_verify(args, rank, world, device, dist):
            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
            "data": "tests/golden/400kb.txt x 5 per file (the reference's perf-test files)",
            "config": {"workload": "verify-on-load of 1000 x 2,068,480-B chunk files (CRC region "
-                                  f"{region} B each), open/mmap/munmap included", "files": files,
+                                  f"{region} B each), open/pread/close included", "files": files,
                       "file_bytes": fsize},
            "check": check}
     if cpu is not None:
