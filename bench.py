@@ -469,14 +469,13 @@ def run_e2e(args, rank, world, device, dist):
     from chunkio_amd import workloads as wl
     lens, ids, seed, desc, scaling = geometry("e2e", rank, world)
     host, offs = wl.host_batch(seed, lens, align=16)
-    bufs = [host[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
     for _ in range(max(1, args.warmup)):
-        out = cio.crc32_batch_host(bufs)
+        out = cio.crc32_batch_host_packed(host, offs, lens)
     barrier(dist)
     t0 = time.perf_counter()
     steps = max(1, min(args.steps, 10))
     for _ in range(steps):
-        out = cio.crc32_batch_host(bufs)
+        out = cio.crc32_batch_host_packed(host, offs, lens)
     barrier(dist)
     elapsed = max_over_ranks(time.perf_counter() - t0, dist, device)
     value = int(lens.sum()) * world * steps / elapsed / 1e9
@@ -487,11 +486,11 @@ def run_e2e(args, rank, world, device, dist):
     reg_ms = (time.perf_counter() - treg) * 1e3
     try:
         for _ in range(max(1, args.warmup)):
-            out_reg = cio.crc32_batch_host(bufs)
+            out_reg = cio.crc32_batch_host_packed(host, offs, lens)
         barrier(dist)
         t0 = time.perf_counter()
         for _ in range(steps):
-            out_reg = cio.crc32_batch_host(bufs)
+            out_reg = cio.crc32_batch_host_packed(host, offs, lens)
         barrier(dist)
         elapsed_reg = max_over_ranks(time.perf_counter() - t0, dist, device)
     finally:

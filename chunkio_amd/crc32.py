@@ -178,6 +178,35 @@ def crc32_batch_host(bufs, seeds=None, devices=None):
     return out[:n]
 
 
+def crc32_batch_host_packed(host, offs, lens, seeds=None, devices=None):
+    """crc32_batch_host over chunks packed in ONE host array: chunk i is
+    host[offs[i]:offs[i] + lens[i]].  The pointer array is built with one numpy
+    add instead of a Python object per chunk (the C call is the same)."""
+    host = np.ascontiguousarray(host).view(np.uint8).reshape(-1)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    n = len(lens)
+    if n and int((offs + lens).max()) > host.size:
+        raise ValueError("crc32_batch_host_packed: chunk past the end of the host array")
+    ptrs = offs + np.uint64(host.ctypes.data)
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    seeds_p = None
+    if seeds is not None:
+        seeds_arr = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint32))
+        seeds_p = seeds_arr.ctypes.data_as(_lib.c_u32_p)
+    P = ctypes.POINTER
+    pp = ptrs.ctypes.data_as(P(ctypes.c_void_p))
+    lp = lens.ctypes.data_as(P(ctypes.c_size_t))
+    op = out.ctypes.data_as(_lib.c_u32_p)
+    if devices:
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _lib.check(_lib.lib().cio_crc32_batch_host_multi(pp, lp, seeds_p, op, n, devs, len(devices)),
+                   "cio_crc32_batch_host_multi")
+    else:
+        _lib.check(_lib.lib().cio_crc32_batch_host(pp, lp, seeds_p, op, n), "cio_crc32_batch_host")
+    return out[:n]
+
+
 def device_count():
     """Visible GPUs (cio_gpu_device_count)."""
     return int(_lib.lib().cio_gpu_device_count())

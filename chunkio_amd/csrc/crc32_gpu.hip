@@ -1874,6 +1874,23 @@ static size_t stage_bytes()
     return v;
 }
 #define kStage (stage_bytes())
+
+// Capacity of a call's first staging group (CIO_GPU_STAGE_FIRST_MB, default 4);
+// each later group doubles it up to kStage.
+static size_t first_stage_bytes()
+{
+    static const size_t v = [] {
+        size_t mb = 4;
+        if (const char *r = getenv("CIO_GPU_STAGE_FIRST_MB")) {
+            const long x = atol(r);
+            if (x >= 1 && x <= 1024) {
+                mb = (size_t) x;
+            }
+        }
+        return mb << 20;
+    }();
+    return v;
+}
 constexpr int kSlots = 3;
 
 // One staging group.  A source is host memory (src[k]) or, for batches read
@@ -2288,20 +2305,24 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     }
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    // Groups of <= kStage bytes, 16-byte aligned segment placement.
+    // Groups of <= kStage bytes, 16-byte aligned segment placement.  The
+    // first groups are smaller (first_stage_bytes(), doubling up to kStage):
+    // the DMA engine starts after a short copy instead of a full slot's.
     std::vector<HostGroup> groups(1);
+    uint64_t cap = std::min<uint64_t>(first_stage_bytes(), kStage);
     for (size_t i = 0; i < n; i++) {
         const uint8_t *p = fds ? nullptr : reinterpret_cast<const uint8_t *>(bufs[i]);
         uint64_t left = lens[i], done = 0;
         do {
             HostGroup *g = &groups.back();
             uint64_t at = (g->bytes + 15) & ~15ull;
-            if (at >= kStage) {
+            if (at >= cap) {
                 groups.emplace_back();
                 g = &groups.back();
                 at = 0;
+                cap = std::min<uint64_t>(cap * 2, kStage);
             }
-            const uint64_t take = std::min<uint64_t>(left, kStage - at);
+            const uint64_t take = std::min<uint64_t>(left, cap - at);
             if (fds) {
                 g->fd.push_back(fds[i]);
                 g->foff.push_back(foffs[i] + done);
@@ -2337,10 +2358,10 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     // Every slot is idle between calls (the previous call synchronised them).
     e = grow_dev(&hp->state, &hp->state_cap, n, false, s0.stream);
     if (e == hipSuccess) {
+        // Ordered before every kernel: group 0 runs on slot 0's stream after
+        // it, and each later group's kernel waits for the previous one's.
+        // (init outlives the call's final synchronisation.)
         e = hipMemcpyAsync(hp->state, init.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s0.stream);
-    }
-    if (e == hipSuccess) {
-        e = hipStreamSynchronize(s0.stream);
     }
     std::shared_lock<std::shared_mutex> rlk(g_reg_mu);
     int rc = CIO_OK;

@@ -281,6 +281,23 @@ def test_host_batch_end_to_end(cuda, data400):
     assert int(got0[0]) ^ INIT == 0x103CFA67
 
 
+def test_host_batch_packed_and_graduated_groups(cuda):
+    # One packed host array through crc32_batch_host_packed (pointer array
+    # built in numpy); sizes straddle the graduated first groups (4, 8, 16 ...
+    # MiB) and one chunk spans several of them.
+    rng = np.random.default_rng(13)
+    lens = rng.integers(0, 3_000_000, 120).astype(np.uint64)
+    lens[7] = 40 * 1024 * 1024 + 3
+    lens[::17] = rng.integers(0, 4, len(lens[::17]))
+    host, offs = wl.host_batch(0x9AC, lens, align=1)
+    seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+    want = po.crc_batch(host, offs, lens, seeds=seeds)
+    np.testing.assert_array_equal(cio.crc32_batch_host_packed(host, offs, lens, seeds=seeds), want)
+    np.testing.assert_array_equal(cio.crc32_batch_host_packed(host, offs, lens, seeds=seeds, devices=[0, 0]), want)
+    bufs = [host[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
+    np.testing.assert_array_equal(cio.crc32_batch_host(bufs, seeds=seeds), want)
+
+
 @pytest.mark.gpu
 def test_host_pipeline_reuse_and_growth(cuda):
     """The persistent host pipeline across calls whose shapes grow and shrink
