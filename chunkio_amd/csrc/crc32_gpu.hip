@@ -1942,7 +1942,9 @@ public:
         const uint64_t npieces = (g.bytes + kPiece - 1) / kPiece;
         if (npieces <= 1 || workers_.empty()) {
             before();
-            return range(dst, g, 0, g.bytes);
+            const bool ok = range(dst, g, 0, g.bytes);
+            cioa_stage_fence();
+            return ok;
         }
         {
             std::lock_guard<std::mutex> lk(mu_);
@@ -1957,6 +1959,7 @@ public:
         cv_.notify_all();
         before();
         const bool ok = drain(dst, g, npieces);
+        cioa_stage_fence();
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [this] { return pending_ == 0; });
         return ok && !failed_;
@@ -1988,7 +1991,7 @@ private:
                 continue;
             }
             if (g.fd.empty()) {
-                memcpy(dst + x, g.src[k] + (x - a), y - x);
+                cioa_stage_copy(dst + x, g.src[k] + (x - a), y - x);
                 continue;
             }
             uint64_t done = 0;
@@ -2026,6 +2029,7 @@ private:
                 npieces = npieces_;
             }
             const bool ok = drain(dst, *g, npieces);
+            cioa_stage_fence();
             std::lock_guard<std::mutex> lk(mu_);
             failed_ = failed_ || !ok;
             if (--pending_ == 0) {

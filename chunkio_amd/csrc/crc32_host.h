@@ -19,6 +19,11 @@ void cioa_gen_slice4(uint32_t out[4][256]);
 void cioa_gen_shift_table(uint32_t out[4][256], uint64_t dist);
 void cioa_gen_xpow8_table(uint32_t *out, size_t count, uint64_t unit_bytes);
 
+/* Copy into pinned staging (non-temporal stores where the CPU has AVX2);
+ * cioa_stage_fence() before publishing the copied bytes to another thread. */
+void cioa_stage_copy(void *dst, const void *src, size_t n);
+void cioa_stage_fence(void);
+
 /* Record an error message for cio_gpu_last_error(); returns CIO_ERROR (-1). */
 int cioa_fail_msg(const char *what, const char *detail);
 
