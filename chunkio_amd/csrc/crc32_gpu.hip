@@ -1977,6 +1977,12 @@ private:
             ok &= range(dst, g, p * kPiece, std::min<uint64_t>(g.bytes, (p + 1) * kPiece));
         }
     }
+    static constexpr uint64_t kBounce = 256u << 10;
+    static uint8_t *bounce_buffer()
+    {
+        thread_local std::unique_ptr<uint8_t[]> b(new uint8_t[kBounce]);
+        return b.get();
+    }
     // Bytes [lo, hi) of the group's staging image.
     static bool range(uint8_t *dst, const HostGroup &g, uint64_t lo, uint64_t hi)
     {
@@ -1994,16 +2000,24 @@ private:
                 cioa_stage_copy(dst + x, g.src[k] + (x - a), y - x);
                 continue;
             }
+            // File source: pread through a per-thread, cache-resident bounce
+            // buffer, then the streaming copy into staging -- a pread straight
+            // into the pinned image would read every destination line first.
+            uint8_t *bounce = cioa_stage_nt() ? bounce_buffer() : nullptr;
             uint64_t done = 0;
             while (done < y - x) {
-                const ssize_t r = pread(g.fd[k], dst + x + done, y - x - done,
-                                        (off_t) (g.foff[k] + (x - a) + done));
+                uint8_t *to = bounce ? bounce : dst + x + done;
+                const uint64_t want = bounce ? std::min<uint64_t>(y - x - done, kBounce) : y - x - done;
+                const ssize_t r = pread(g.fd[k], to, want, (off_t) (g.foff[k] + (x - a) + done));
                 if (r <= 0) {
                     if (r < 0 && errno == EINTR) {
                         continue;
                     }
                     ok = false;
                     break;
+                }
+                if (bounce) {
+                    cioa_stage_copy(dst + x + done, bounce, (size_t) r);
                 }
                 done += (uint64_t) r;
             }

@@ -22,6 +22,7 @@ void cioa_gen_xpow8_table(uint32_t *out, size_t count, uint64_t unit_bytes);
 /* Copy into pinned staging (non-temporal stores where the CPU has AVX2);
  * cioa_stage_fence() before publishing the copied bytes to another thread. */
 void cioa_stage_copy(void *dst, const void *src, size_t n);
+int cioa_stage_nt(void);            /* 1 when cioa_stage_copy uses streaming stores */
 void cioa_stage_fence(void);
 
 /* Record an error message for cio_gpu_last_error(); returns CIO_ERROR (-1). */

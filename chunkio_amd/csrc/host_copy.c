@@ -48,6 +48,11 @@ static int nt_enabled(void)
     return v;
 }
 
+__attribute__((visibility("hidden"))) int cioa_stage_nt(void)
+{
+    return nt_enabled();
+}
+
 __attribute__((visibility("hidden"))) void cioa_stage_copy(void *dst, const void *src, size_t n)
 {
     if (n >= 4096 && nt_enabled()) {
