@@ -1116,8 +1116,11 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
 // 4 KiB wave-steps and the same coalesced non-temporal 16-byte loads, with the
 // CRC replaced by an XOR.  One 4-byte store per wave keeps the loads live.
 __global__ void __launch_bounds__(kThreads, 1)
-read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__restrict__ sink, uint32_t B)
+read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__restrict__ sink, uint32_t B,
+                   unsigned long long *stamps)
 {
+    const unsigned long long t_entry = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long t_first = 0;
     const uint32_t W = gridDim.x * (kThreads / kWave);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
@@ -1165,6 +1168,10 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
         const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
         for (uint64_t g = g0; g < g1; ++g) {
             step(g);
+            if (stamps && g == g0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                t_first = __builtin_amdgcn_s_memrealtime();
+            }
         }
     } else {
         // diagnostic (CIO_GPU_RS_BLOCK=B): blocks of B steps dealt round-robin over the waves
@@ -1177,6 +1184,15 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
     const uint32_t x = wave_xor(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]);
     if (lane == 0) {
         sink[wave] = x;
+    }
+    if (stamps && lane == 0) {
+        // Diagnostic (CIO_GPU_RS_STAMPS=1): 100 MHz global clock, per wave.
+        uint32_t xcc_id;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+        stamps[4 * wave + 0] = t_entry;
+        stamps[4 * wave + 1] = t_first;
+        stamps[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+        stamps[4 * wave + 3] = xcc_id;
     }
 }
 
@@ -1765,6 +1781,24 @@ int cio_gpu_fill_synthetic(void *dev_base, const uint64_t *offs, const uint64_t 
     return CIO_OK;
 }
 
+static unsigned long long *g_rs_stamps = nullptr;   // CIO_GPU_RS_STAMPS diagnostic
+static uint32_t g_rs_waves = 0;
+
+/* Diagnostic (not in the public header): per-wave (entry, first step, done,
+ * xcc) stamps of the last CIO_GPU_RS_STAMPS=1 read-stream launch; returns the
+ * number of waves. */
+int cioa_debug_rs_stamps(unsigned long long *host, size_t cap)
+{
+    if (!g_rs_stamps) {
+        return 0;
+    }
+    const size_t n = std::min(cap, (size_t) g_rs_waves * 4);
+    if (hipMemcpy(host, g_rs_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) {
+        return 0;
+    }
+    return (int) g_rs_waves;
+}
+
 int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
 {
     DeviceState *st;
@@ -1783,9 +1817,19 @@ int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
     if (const char *r = getenv("CIO_GPU_RS_BLOCK")) {
         B = (uint32_t) atoi(r);
     }
+    unsigned long long *stamps = nullptr;
+    if (const char *r = getenv("CIO_GPU_RS_STAMPS")) {
+        if (atoi(r) > 0) {
+            if (!g_rs_stamps) {
+                HIP_TRY(hipMalloc(&g_rs_stamps, 65536 * 4 * sizeof(unsigned long long)), "read_stream: hipMalloc");
+            }
+            stamps = g_rs_stamps;
+            g_rs_waves = st->cus * (kThreads / kWave);
+        }
+    }
     hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream),
-                       reinterpret_cast<const uint8_t *>(dev_base), S, sink, B);
+                       reinterpret_cast<const uint8_t *>(dev_base), S, sink, B, stamps);
     HIP_TRY(hipGetLastError(), "read_stream_kernel launch");
     return CIO_OK;
 }
