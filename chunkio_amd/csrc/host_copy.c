@@ -43,6 +43,7 @@ static int nt_enabled(void)
     static int v = -1;
     if (v < 0) {
         const char *r = getenv("CIO_GPU_NT_COPY");
+        __builtin_cpu_init();
         v = (r == NULL || atoi(r) != 0) && __builtin_cpu_supports("avx2");
     }
     return v;
