@@ -230,9 +230,10 @@ __device__ __forceinline__ uint32_t byte_step(const char *lds, uint32_t lb_lo, u
 __device__ __forceinline__ uint32_t step_shift(const char *lds, uint32_t lrep, uint32_t s)
 {
     const char *t = lds + kShiftOff + lrep;
-    return *reinterpret_cast<const uint32_t *>(t + (s & 0xffu) * 32u) ^
-           *reinterpret_cast<const uint32_t *>(t + 8192 + ((s >> 8) & 0xffu) * 32u) ^
-           *reinterpret_cast<const uint32_t *>(t + 16384 + ((s >> 16) & 0xffu) * 32u) ^
+    return __builtin_amdgcn_bitop3_b32(*reinterpret_cast<const uint32_t *>(t + (s & 0xffu) * 32u),
+                                       *reinterpret_cast<const uint32_t *>(t + 8192 + ((s >> 8) & 0xffu) * 32u),
+                                       *reinterpret_cast<const uint32_t *>(t + 16384 + ((s >> 16) & 0xffu) * 32u),
+                                       0x96) ^
            *reinterpret_cast<const uint32_t *>(t + 24576 + (s >> 24) * 32u);
 }
 
@@ -246,15 +247,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 // the 16 bytes of v.  The four lookups of every word and the next data word
 // are combined with two 3-input XORs (10 XOR instructions per 16 bytes
 // instead of 19).
-__device__ __forceinline__ uint32_t shift_block16(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
-                                                  uint32_t lrep, uint32_t s, const uint4 &v)
+// crc_update(h, the 16 bytes of v): four dependent rounds of four lookups.
+__device__ __forceinline__ uint32_t block16(const char *lds, uint32_t lb_lo, uint32_t lb_hi, uint32_t h,
+                                            const uint4 &v)
 {
-    const char *t = lds + kShiftOff + lrep;
-    const uint32_t h0 = *reinterpret_cast<const uint32_t *>(t + (s & 0xffu) * 32u);
-    const uint32_t h1 = *reinterpret_cast<const uint32_t *>(t + 8192 + ((s >> 8) & 0xffu) * 32u);
-    const uint32_t h2 = *reinterpret_cast<const uint32_t *>(t + 16384 + ((s >> 16) & 0xffu) * 32u);
-    const uint32_t h3 = *reinterpret_cast<const uint32_t *>(t + 24576 + (s >> 24) * 32u);
-    uint32_t x = xor3(xor3(h0, h1, h2), h3, v.x);
+    uint32_t x = h ^ v.x;
     const uint32_t w[3] = {v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -263,6 +260,12 @@ __device__ __forceinline__ uint32_t shift_block16(const char *lds, uint32_t lb_l
     }
     return xor3(tl<3>(lds, lb_hi, x, 0), tl<2>(lds, lb_hi, x, 1), tl<1>(lds, lb_lo, x, 2)) ^
            tl<0>(lds, lb_lo, x, 3);
+}
+
+__device__ __forceinline__ uint32_t shift_block16(const char *lds, uint32_t lb_lo, uint32_t lb_hi,
+                                                  uint32_t lrep, uint32_t s, const uint4 &v)
+{
+    return block16(lds, lb_lo, lb_hi, step_shift(lds, lrep, s), v);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -700,12 +703,21 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         auto crc_step = [&](StepRegs &r) -> bool {
             {
                 if (j < full_end) {
+                    // The 4080-byte jump of every sub-chain needs only its
+                    // state: its lookups go out before the first use of the
+                    // step's data, so after the data lands only the four
+                    // rounds of the 16-byte update remain.
+                    uint32_t h[kSub];
+#pragma unroll
+                    for (int q = 0; q < kSub; ++q) {
+                        h[q] = step_shift(lds, lrep, s[q]);
+                    }
                     if (j == 0) {
                         r.q[0] = head_fix(r.q[0], lane, d.h, seed);
                     }
 #pragma unroll
                     for (int q = 0; q < kSub; ++q) {
-                        s[q] = shift_block16(lds, lb_lo, lb_hi, lrep, s[q], r.q[q]);
+                        s[q] = block16(lds, lb_lo, lb_hi, h[q], r.q[q]);
                     }
                     const uint64_t e0 = j * kStep + (uint64_t) (lane + 1) * kGran;
 #pragma unroll
@@ -1117,7 +1129,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
 // CRC replaced by an XOR.  One 4-byte store per wave keeps the loads live.
 __global__ void __launch_bounds__(kThreads, 1)
 read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__restrict__ sink, uint32_t B,
-                   unsigned long long *stamps)
+                   unsigned long long *stamps, uint32_t work)
 {
     const unsigned long long t_entry = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long t_first = 0;
@@ -1125,12 +1137,26 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
     u32x4 acc = {0u, 0u, 0u, 0u};
+    // diagnostic (CIO_GPU_RS_WORK=n): n rounds of 4 independent dependent
+    // chains of full-rate VALU work (3 instructions per chain and round) on
+    // each step's data, standing in for the CRC's arithmetic.
+    auto burn = [&]() {
+        uint32_t x0 = acc.x, x1 = acc.y, x2 = acc.z, x3 = acc.w;
+        for (uint32_t k = 0; k < work; ++k) {
+            x0 = __builtin_amdgcn_alignbit(x0, x0, 27) ^ (x0 + k);
+            x1 = __builtin_amdgcn_alignbit(x1, x1, 27) ^ (x1 + k);
+            x2 = __builtin_amdgcn_alignbit(x2, x2, 27) ^ (x2 + k);
+            x3 = __builtin_amdgcn_alignbit(x3, x3, 27) ^ (x3 + k);
+        }
+        acc = u32x4{x0, x1, x2, x3};
+    };
     auto step = [&](uint64_t g) {
         const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * kGran);
 #pragma unroll
         for (int q = 0; q < kSub; ++q) {
             acc ^= __builtin_nontemporal_load(p + q * kWave);
         }
+        burn();
     };
     if (B == 0xffffffffu) {
         // diagnostic (CIO_GPU_RS_BLOCK=-1): the contiguous split with two
@@ -1155,12 +1181,14 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
                 }
                 ld4(ra, g + 2);
                 __builtin_amdgcn_sched_barrier(0);
+                burn();
 #pragma unroll
                 for (int q = 0; q < kSub; ++q) {
                     acc ^= rb[q];
                 }
                 ld4(rb, g + 3);
                 __builtin_amdgcn_sched_barrier(0);
+                burn();
             }
         }
     } else if (B == 0) {
@@ -1827,9 +1855,13 @@ int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
             g_rs_waves = st->cus * (kThreads / kWave);
         }
     }
+    uint32_t work = 0;
+    if (const char *r = getenv("CIO_GPU_RS_WORK")) {
+        work = (uint32_t) std::max(0, atoi(r));
+    }
     hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream),
-                       reinterpret_cast<const uint8_t *>(dev_base), S, sink, B, stamps);
+                       reinterpret_cast<const uint8_t *>(dev_base), S, sink, B, stamps, work);
     HIP_TRY(hipGetLastError(), "read_stream_kernel launch");
     return CIO_OK;
 }
