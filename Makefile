@@ -15,7 +15,7 @@ HIPFLAGS := -O3 -fPIC --offload-arch=$(ARCH) -std=c++17 -Wall $(INC) -munsafe-fp
             -mllvm -amdgpu-atomic-optimizer-strategy=None -mllvm -amdgpu-kernarg-preload-count=8
 
 COBJS   := $(BLD)/host_copy.o $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o $(BLD)/cioa_chunk.o
-HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/sha1_gpu.o
+HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/host_pipeline.o $(BLD)/sha1_gpu.o
 
 CTEST   := tests/c/bin
 REF_INC := /root/reference/include/chunkio/cio_crc32.h
@@ -60,7 +60,7 @@ oracle:
 ablib:
 	@mkdir -p $(OUT)/ab $(BLD)/ab
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(BLD)/ab/crc32_gpu_$(VAR).o $(SRC)/crc32_gpu.hip
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(OUT)/ab/$(VAR).so $(COBJS) $(BLD)/ab/crc32_gpu_$(VAR).o $(BLD)/sha1_gpu.o -lpthread
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(OUT)/ab/$(VAR).so $(COBJS) $(BLD)/ab/crc32_gpu_$(VAR).o $(BLD)/host_pipeline.o $(BLD)/sha1_gpu.o -lpthread
 
 asm: $(SRC)/crc32_gpu.hip
 	@mkdir -p $(BLD)/asm

@@ -804,7 +804,7 @@ def other_configs(args, rank, world, device, dist):
     import torch
     out = {}
     t0 = time.perf_counter()
-    for cfg, steps, warm in (("cfg3", 5, 2), ("sha1", 10, 2), ("e2e", 5, 1)):
+    for cfg, steps, warm in (("cfg3", 5, 2), ("sha1", 10, 2), ("e2e", 10, 10)):
         torch.cuda.empty_cache()
         a = copy.copy(args)
         a.config, a.steps, a.warmup, a.no_cpu = cfg, steps, warm, True

@@ -44,44 +44,11 @@
 #include <string>
 #include <algorithm>
 
-#include "crc32_host.h"
-#include "chunkio_amd/cio_crc32_gpu.h"
+#include "cio_gpu_internal.h"
+
+using namespace cioa;
 
 namespace {
-
-constexpr int kWave = 64;
-constexpr int kGran = 16;                   // bytes per lane per sub-chain per step
-constexpr int kSub = 4;                     // sub-chains per lane
-constexpr int kRow = kWave * kGran;         // 1024: one coalesced wave-instruction
-constexpr int kStep = kSub * kRow;          // 4096 bytes per wave-step
-constexpr int kThreads = 1024;              // one workgroup per CU
-constexpr int kX8Count = 2 * kStep;         // x^(8m), m in [0, 8192)
-constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
-constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
-constexpr uint32_t kShiftOff = kSliceBytes;
-constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
-constexpr int kStampWords = 12;
-              // diagnostic stamps per wave (CIO_GPU_STAMPS)
-
-struct ChunkDesc {
-    uint64_t a;        // aligned-down start offset from the batch base
-    uint64_t vlen;     // virtual length = (off & 15) + len
-    uint64_t g;        // first global wave-step of this chunk
-    uint32_t nsteps;   // ceil(vlen / kStep); 0 for tiny chunks (len < 4)
-    uint32_t h;        // off & 15 (zeroed head bytes)
-    uint32_t npieces;  // waves holding a piece of this chunk
-    uint32_t pad[3];
-};
-static_assert(sizeof(ChunkDesc) == 48, "desc layout");
-
-// Where each wave's step range begins: its first chunk and that chunk's
-// descriptor, so a wave starts streaming after ONE scalar load.
-struct WaveStart {
-    ChunkDesc d;
-    uint32_t c;
-    uint32_t pad[3];
-};
-static_assert(sizeof(WaveStart) == 64, "wave start layout");
 
 // ---------------------------------------------------------------- device math
 
@@ -1280,9 +1247,13 @@ fill_kernel(uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
 
 // ---------------------------------------------------------------- host side
 
+}  // namespace
+
+namespace cioa {
+
 thread_local std::string g_err;
 
-int fail(const char *what, hipError_t e = hipSuccess)
+int fail(const char *what, hipError_t e)
 {
     char buf[512];
     if (e != hipSuccess) {
@@ -1294,7 +1265,7 @@ int fail(const char *what, hipError_t e = hipSuccess)
     return CIO_ERROR;
 }
 
-}  // namespace
+}  // namespace cioa
 
 extern "C" int cioa_fail_msg(const char *what, const char *detail)
 {
@@ -1302,27 +1273,11 @@ extern "C" int cioa_fail_msg(const char *what, const char *detail)
     return CIO_ERROR;
 }
 
-namespace {
-
-#define HIP_TRY(expr, what)                         \
-    do {                                            \
-        hipError_t e_ = (expr);                     \
-        if (e_ != hipSuccess) return fail(what, e_); \
-    } while (0)
-
-struct DeviceState {
-    bool ready = false;
-    int cus = 0;
-    uint32_t *slice = nullptr;   // [4][256] compact
-    uint32_t *shift = nullptr;   // [4][256] shift by kStep - kBPL
-    uint32_t *x8 = nullptr;      // [kX8Count]
-    uint32_t *xinv8 = nullptr;   // [kStep]: x^(-8 d) (d bytes un-shifted)
-};
+namespace cioa {
 
 // One DeviceState per HIP device, allocated once and never moved: plans and
 // in-flight host batches keep a pointer to it (a growing vector
 // here reallocated under them when a second device was first used).
-constexpr int kMaxDev = 64;
 std::mutex g_mu;
 std::unique_ptr<DeviceState> g_dev[kMaxDev];
 
@@ -1379,29 +1334,7 @@ int device_state(DeviceState **out)
     return CIO_OK;
 }
 
-}  // namespace
-
-
-struct cio_crc32_plan {
-    uint32_t n = 0;
-    uint64_t S = 0;            // total wave-steps
-    uint32_t W = 0;            // waves in the grid
-    uint32_t grid = 0;         // workgroups
-    uint32_t ntiny = 0;        // chunks with len < 4 (byte-serial)
-    int prio = 1;              // CIO_GPU_PRIO: 0 none, 1 per-step rotation (2/3, time-sliced, measured slower and removed)
-    uint64_t ustride = 0, ua0 = 0, uvlen = 0;   // uniform batch geometry (unsteps > 0)
-    uint32_t unsteps = 0, uh = 0;
-    bool small = false;        // every chunk fits one wave-step: crc32_small_kernel
-    unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
-    uint64_t bytes = 0;        // sum of lens
-    ChunkDesc *desc = nullptr;
-    WaveStart *wstart = nullptr;
-    uint32_t *tiny = nullptr;
-    unsigned long long *partials = nullptr;
-    uint32_t *counters = nullptr;
-    uint32_t *pfac = nullptr;   // per piece slot: x^(8 * chunk bytes after the piece)
-    DeviceState *st = nullptr;
-};
+}  // namespace cioa
 
 extern "C" {
 
@@ -1438,7 +1371,7 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
 
 }  // extern "C"
 
-namespace {
+namespace cioa {
 
 // Tuning knobs (environment, read at plan creation) and grid geometry.
 void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
@@ -1452,15 +1385,6 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     p->grid = (uint32_t) st->cus;
     p->W = p->grid * (kThreads / kWave);
 }
-
-// Host image of everything a launch reads besides the data.
-struct PlanHost {
-    std::vector<ChunkDesc> desc;
-    std::vector<WaveStart> ws;
-    std::vector<uint32_t> tiny;
-    std::vector<uint32_t> pfac;   // per piece slot (wave + chunk)
-    uint64_t S = 0, bytes = 0;
-};
 
 // Virtual aligned chunks, wave-step numbering, the even split of the S steps
 // over W waves, each wave's first chunk, per-chunk piece counts and per-slot
@@ -1554,6 +1478,10 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
     }
     return nullptr;
 }
+
+}  // namespace cioa
+
+namespace {
 
 // Uniform batch: n equal lengths >= 4 at offsets off0 + i * stride with
 // stride a multiple of 16 (every chunk has the same misalignment).  The
@@ -1670,9 +1598,6 @@ const char *cio_crc32_plan_kernel(const cio_crc32_plan *p)
     return (p && p->small) ? "crc32_small_kernel" : "crc32_stream_kernel";
 }
 
-static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const uint32_t *dev_seeds,
-                          uint32_t *dev_out, const uint32_t *cid, hipStream_t s,
-                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 int cio_crc32_plan_exec_events(const cio_crc32_plan *p, const void *dev_base,
                                const uint32_t *dev_seeds, uint32_t *dev_out, void *stream,
@@ -1713,9 +1638,9 @@ static StreamKernel select_kernel(int prio, bool stamps, bool uniform)
 // One launch: stream kernel (CRC of every step, per-chunk fold by the last
 // arriver, tiny chunks).  The per-chunk counters are self-resetting, so no
 // memset node precedes it and the launch can be captured in a HIP graph.
-static int plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const uint32_t *dev_seeds,
-                          uint32_t *dev_out, const uint32_t *cid, hipStream_t s,
-                          hipEvent_t ev0, hipEvent_t ev1)
+int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const uint32_t *dev_seeds,
+                         uint32_t *dev_out, const uint32_t *cid, hipStream_t s,
+                         hipEvent_t ev0, hipEvent_t ev1)
 {
     if (!p) {
         return fail("cio_crc32_plan_exec: null plan");
@@ -1910,850 +1835,3 @@ int cio_gpu_stream_sync(void *stream)
 
 }  // extern "C"
 
-// ---------------------------------------------------------------- host-memory batch
-//
-// End-to-end path for chunks that live in host memory (mmap'd chunk files,
-// src/cio_file_unix.c:100).  The batch is cut into segments of at most kStage
-// bytes packed into groups.  A persistent per-device pipeline of kSlots slots
-// (pinned staging buffer, pinned plan image, device buffer, device plan
-// arena, stream) carries the groups: host threads copy group g into a free
-// slot while the DMA engine moves group g-1 and the GPU CRCs group g-2.  Each
-// group's plan is built on the host straight into the slot's pinned image and
-// uploaded with the data, so steady-state calls allocate nothing.  Seeds and
-// outputs go through a chunk-id map into one running-state array on the
-// device, so a chunk split over several groups chains its state on the GPU.
-
-#include <atomic>
-#include <thread>
-#include <condition_variable>
-#include <errno.h>
-#include <time.h>
-#include <unistd.h>
-
-namespace {
-
-// Slot size: CIO_GPU_STAGE_MB (read once, when the pipeline is created),
-// default 64 MiB.  Smaller groups shorten the pipeline's fill and drain (the
-// first group's host copy and the last group's DMA are not overlapped).
-static size_t stage_bytes()
-{
-    static const size_t v = [] {
-        size_t mb = 64;
-        if (const char *r = getenv("CIO_GPU_STAGE_MB")) {
-            const long x = atol(r);
-            if (x >= 1 && x <= 1024) {
-                mb = (size_t) x;
-            }
-        }
-        return mb << 20;
-    }();
-    return v;
-}
-#define kStage (stage_bytes())
-
-// Capacity of a call's first staging group (CIO_GPU_STAGE_FIRST_MB, default 4);
-// each later group doubles it up to kStage.
-static size_t first_stage_bytes()
-{
-    static const size_t v = [] {
-        size_t mb = 4;
-        if (const char *r = getenv("CIO_GPU_STAGE_FIRST_MB")) {
-            const long x = atol(r);
-            if (x >= 1 && x <= 1024) {
-                mb = (size_t) x;
-            }
-        }
-        return mb << 20;
-    }();
-    return v;
-}
-constexpr int kSlots = 3;
-
-// One staging group.  A source is host memory (src[k]) or, for batches read
-// straight from files, a file range (fd[k], foff[k]) that the copy threads
-// pread() into the pinned buffer: no mapping, no page faults, no TLB
-// shootdowns at unmap.
-struct HostGroup {
-    std::vector<const uint8_t *> src;
-    std::vector<int> fd;               // empty for memory sources
-    std::vector<uint64_t> foff;
-    std::vector<uint64_t> offs, lens;
-    std::vector<uint32_t> cid;
-    uint64_t bytes = 0;
-};
-
-// Persistent host copy workers (the box's CPU share per GPU is 16 threads).
-// copy() cuts a group's byte range into 1 MiB pieces that the workers and
-// the caller claim through one atomic counter, so a slow or descheduled
-// thread delays the group by one piece, not by a 1/16 slice.  The caller
-// first runs `before` (the group's plan build), overlapping it with the
-// workers' copying.
-class CopyPool {
-public:
-    static constexpr uint64_t kPiece = 1ull << 20;
-
-    CopyPool()
-    {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const unsigned nw = std::min(15u, hw > 1 ? hw - 1 : 0u);
-        for (unsigned t = 0; t < nw; t++) {
-            workers_.emplace_back([this]() { run(); });
-        }
-    }
-    ~CopyPool()
-    {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &w : workers_) {
-            w.join();
-        }
-    }
-    // false if a file source could not be read in full
-    template <typename F>
-    bool copy(uint8_t *dst, const HostGroup &g, F before)
-    {
-        const uint64_t npieces = (g.bytes + kPiece - 1) / kPiece;
-        if (npieces <= 1 || workers_.empty()) {
-            before();
-            const bool ok = range(dst, g, 0, g.bytes);
-            cioa_stage_fence();
-            return ok;
-        }
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            dst_ = dst;
-            g_ = &g;
-            npieces_ = npieces;
-            next_.store(0, std::memory_order_relaxed);
-            pending_ = workers_.size();
-            failed_ = false;
-            ++gen_;
-        }
-        cv_.notify_all();
-        before();
-        const bool ok = drain(dst, g, npieces);
-        cioa_stage_fence();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return pending_ == 0; });
-        return ok && !failed_;
-    }
-
-private:
-    bool drain(uint8_t *dst, const HostGroup &g, uint64_t npieces)
-    {
-        bool ok = true;
-        for (;;) {
-            const uint64_t p = next_.fetch_add(1, std::memory_order_relaxed);
-            if (p >= npieces) {
-                return ok;
-            }
-            ok &= range(dst, g, p * kPiece, std::min<uint64_t>(g.bytes, (p + 1) * kPiece));
-        }
-    }
-    static constexpr uint64_t kBounce = 256u << 10;
-    static uint8_t *bounce_buffer()
-    {
-        thread_local std::unique_ptr<uint8_t[]> b(new uint8_t[kBounce]);
-        return b.get();
-    }
-    // Bytes [lo, hi) of the group's staging image.
-    static bool range(uint8_t *dst, const HostGroup &g, uint64_t lo, uint64_t hi)
-    {
-        // first chunk ending after lo (offs increase along the group)
-        size_t k = (size_t) (std::upper_bound(g.offs.begin(), g.offs.end(), lo) - g.offs.begin());
-        k = k ? k - 1 : 0;
-        bool ok = true;
-        for (; k < g.offs.size() && g.offs[k] < hi; k++) {
-            const uint64_t a = g.offs[k], b = a + g.lens[k];
-            const uint64_t x = std::max(a, lo), y = std::min(b, hi);
-            if (x >= y) {
-                continue;
-            }
-            if (g.fd.empty()) {
-                cioa_stage_copy(dst + x, g.src[k] + (x - a), y - x);
-                continue;
-            }
-            // File source: pread through a per-thread, cache-resident bounce
-            // buffer, then the streaming copy into staging -- a pread straight
-            // into the pinned image would read every destination line first.
-            uint8_t *bounce = cioa_stage_nt() ? bounce_buffer() : nullptr;
-            uint64_t done = 0;
-            while (done < y - x) {
-                uint8_t *to = bounce ? bounce : dst + x + done;
-                const uint64_t want = bounce ? std::min<uint64_t>(y - x - done, kBounce) : y - x - done;
-                const ssize_t r = pread(g.fd[k], to, want, (off_t) (g.foff[k] + (x - a) + done));
-                if (r <= 0) {
-                    if (r < 0 && errno == EINTR) {
-                        continue;
-                    }
-                    ok = false;
-                    break;
-                }
-                if (bounce) {
-                    cioa_stage_copy(dst + x + done, bounce, (size_t) r);
-                }
-                done += (uint64_t) r;
-            }
-        }
-        return ok;
-    }
-    void run()
-    {
-        uint64_t seen = 0;
-        for (;;) {
-            uint8_t *dst;
-            const HostGroup *g;
-            uint64_t npieces;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) {
-                    return;
-                }
-                seen = gen_;
-                dst = dst_;
-                g = g_;
-                npieces = npieces_;
-            }
-            const bool ok = drain(dst, *g, npieces);
-            cioa_stage_fence();
-            std::lock_guard<std::mutex> lk(mu_);
-            failed_ = failed_ || !ok;
-            if (--pending_ == 0) {
-                done_cv_.notify_one();
-            }
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    bool stop_ = false;
-    bool failed_ = false;
-    uint64_t gen_ = 0;
-    uint8_t *dst_ = nullptr;
-    const HostGroup *g_ = nullptr;
-    uint64_t npieces_ = 0;
-    std::atomic<uint64_t> next_{0};
-    size_t pending_ = 0;
-};
-
-size_t align256(size_t x)
-{
-    return (x + 255) & ~(size_t) 255;
-}
-
-struct PipeSlot {
-    uint8_t *pinned = nullptr;       // kStage data
-    uint8_t *dbuf = nullptr;         // kStage + 64
-    uint8_t *meta_h = nullptr;       // pinned plan image
-    uint8_t *meta_d = nullptr;       // device plan image
-    size_t meta_cap = 0;
-    unsigned long long *partials = nullptr;
-    size_t part_cap = 0;
-    uint32_t *counters = nullptr;    // zero between launches (self-resetting)
-    size_t cnt_cap = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;       // after the slot's kernel
-    bool busy = false;
-};
-
-struct HostPipe {
-    bool ready = false;
-    CopyPool *pool = nullptr;
-    PipeSlot slot[kSlots];
-    uint32_t *state = nullptr;       // running raw CRC per chunk of the call
-    size_t state_cap = 0;
-};
-
-// Pipelines are pooled per device: a call takes an idle one (or builds one,
-// up to CIO_GPU_PIPES_PER_DEV, default 4) and gives it back when done, so
-// concurrent callers on one device, and callers on different devices, run
-// in parallel.  Nothing global is held while a batch runs.
-struct DevPipes {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::vector<HostPipe *> idle;
-    int count = 0;
-};
-DevPipes g_pipes[kMaxDev];
-
-int pipes_per_dev()
-{
-    static const int v = [] {
-        int k = 4;
-        if (const char *r = getenv("CIO_GPU_PIPES_PER_DEV")) {
-            const int x = atoi(r);
-            if (x >= 1 && x <= 64) {
-                k = x;
-            }
-        }
-        return k;
-    }();
-    return v;
-}
-
-hipError_t pipe_acquire(int dev, HostPipe **out)
-{
-    DevPipes &dp = g_pipes[dev];
-    std::unique_lock<std::mutex> lk(dp.mu);
-    dp.cv.wait(lk, [&] { return !dp.idle.empty() || dp.count < pipes_per_dev(); });
-    if (!dp.idle.empty()) {
-        *out = dp.idle.back();
-        dp.idle.pop_back();
-        return hipSuccess;
-    }
-    dp.count++;
-    *out = new HostPipe();
-    return hipSuccess;
-}
-
-void pipe_release(int dev, HostPipe *hp)
-{
-    DevPipes &dp = g_pipes[dev];
-    {
-        std::lock_guard<std::mutex> lk(dp.mu);
-        dp.idle.push_back(hp);
-    }
-    dp.cv.notify_one();
-}
-
-hipError_t pipe_init(HostPipe &hp)
-{
-    hipError_t e = hipSuccess;
-    for (int b = 0; b < kSlots && e == hipSuccess; b++) {
-        PipeSlot &s = hp.slot[b];
-        if ((e = hipHostMalloc(&s.pinned, kStage, hipHostMallocDefault)) != hipSuccess) break;
-        if ((e = hipMalloc(&s.dbuf, kStage + 64)) != hipSuccess) break;
-        if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess) break;
-        e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-    }
-    if (e == hipSuccess) {
-        hp.pool = new CopyPool();
-    }
-    hp.ready = e == hipSuccess;
-    return e;
-}
-
-template <typename T>
-hipError_t grow_dev(T **p, size_t *cap, size_t need, bool zero, hipStream_t s)
-{
-    if (need <= *cap) {
-        return hipSuccess;
-    }
-    need = std::max(need, *cap * 2);
-    (void) hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    hipError_t e = hipMalloc(p, need * sizeof(T));
-    if (e == hipSuccess && zero) {
-        e = hipMemsetAsync(*p, 0, need * sizeof(T), s);
-    }
-    if (e == hipSuccess) {
-        *cap = need;
-    }
-    return e;
-}
-
-hipError_t grow_meta(PipeSlot &s, size_t need)
-{
-    if (need <= s.meta_cap) {
-        return hipSuccess;
-    }
-    need = std::max(need, s.meta_cap * 2);
-    (void) hipHostFree(s.meta_h);
-    (void) hipFree(s.meta_d);
-    s.meta_h = s.meta_d = nullptr;
-    s.meta_cap = 0;
-    hipError_t e = hipHostMalloc(&s.meta_h, need, hipHostMallocDefault);
-    if (e == hipSuccess) {
-        e = hipMalloc(&s.meta_d, need);
-    }
-    if (e == hipSuccess) {
-        s.meta_cap = need;
-    }
-    return e;
-}
-
-// Build group g's plan into slot s (pinned image + device arenas) and return
-// a launchable plan view over the slot's device memory.
-hipError_t stage_plan(PipeSlot &s, const HostGroup &g, DeviceState *st, cio_crc32_plan &view,
-                      uint32_t **d_cid, size_t *meta_bytes, const char **err)
-{
-    const size_t n = g.offs.size();
-    plan_init(&view, st, n);
-    PlanHost ph;
-    if ((*err = plan_build(ph, g.offs.data(), g.lens.data(), n, view.W)) != nullptr) {
-        return hipSuccess;
-    }
-    const size_t o_desc = 0;
-    const size_t o_ws = o_desc + align256(ph.desc.size() * sizeof(ChunkDesc));
-    const size_t o_tiny = o_ws + align256(ph.ws.size() * sizeof(WaveStart));
-    const size_t o_pfac = o_tiny + align256(std::max<size_t>(1, ph.tiny.size()) * sizeof(uint32_t));
-    const size_t o_cid = o_pfac + align256(ph.pfac.size() * sizeof(uint32_t));
-    const size_t total = o_cid + align256(n * sizeof(uint32_t));
-    hipError_t e = grow_meta(s, total);
-    if (e == hipSuccess) e = grow_dev(&s.partials, &s.part_cap, ph.pfac.size(), false, s.stream);
-    if (e == hipSuccess) e = grow_dev(&s.counters, &s.cnt_cap, std::max<size_t>(1, n), true, s.stream);
-    if (e != hipSuccess) {
-        return e;
-    }
-    memcpy(s.meta_h + o_desc, ph.desc.data(), ph.desc.size() * sizeof(ChunkDesc));
-    memcpy(s.meta_h + o_ws, ph.ws.data(), ph.ws.size() * sizeof(WaveStart));
-    if (!ph.tiny.empty()) {
-        memcpy(s.meta_h + o_tiny, ph.tiny.data(), ph.tiny.size() * sizeof(uint32_t));
-    }
-    memcpy(s.meta_h + o_pfac, ph.pfac.data(), ph.pfac.size() * sizeof(uint32_t));
-    memcpy(s.meta_h + o_cid, g.cid.data(), n * sizeof(uint32_t));
-    view.S = ph.S;
-    view.bytes = ph.bytes;
-    view.ntiny = (uint32_t) ph.tiny.size();
-    view.desc = reinterpret_cast<ChunkDesc *>(s.meta_d + o_desc);
-    view.wstart = reinterpret_cast<WaveStart *>(s.meta_d + o_ws);
-    view.tiny = reinterpret_cast<uint32_t *>(s.meta_d + o_tiny);
-    view.pfac = reinterpret_cast<uint32_t *>(s.meta_d + o_pfac);
-    view.partials = s.partials;
-    view.counters = s.counters;
-    *d_cid = reinterpret_cast<uint32_t *>(s.meta_d + o_cid);
-    *meta_bytes = total;
-    return hipSuccess;
-}
-
-// Host ranges pinned in place by cio_crc32_host_register (long-lived chunk
-// mappings).  A group whose every source lies inside one of them skips the
-// staging copy: the DMA engine reads the caller's pages directly.  Batches
-// hold the registry shared for their whole run (so a range cannot be
-// unregistered under queued DMAs); register/unregister take it exclusively.
-std::shared_mutex g_reg_mu;
-std::vector<std::pair<uintptr_t, size_t>> g_reg;   // (start, length)
-
-bool in_registered(const uint8_t *p, uint64_t len)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    for (const auto &r : g_reg) {
-        if (a >= r.first && a + len <= r.first + r.second) {
-            return true;
-        }
-    }
-    return false;
-}
-
-bool group_registered(const HostGroup &g)
-{
-    if (g_reg.empty() || !g.fd.empty()) {
-        return false;
-    }
-    for (size_t k = 0; k < g.src.size(); k++) {
-        if (g.lens[k] && !in_registered(g.src[k], g.lens[k])) {
-            return false;
-        }
-    }
-    return true;
-}
-
-// Direct DMAs of a registered group into the slot's device buffer, one per
-// run of chunks that are adjacent both in host memory and in the group.
-hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
-{
-    size_t k = 0;
-    while (k < g.src.size()) {
-        if (g.lens[k] == 0) {
-            k++;
-            continue;
-        }
-        const uint8_t *src = g.src[k];
-        const uint64_t at = g.offs[k];
-        uint64_t len = g.lens[k];
-        size_t j = k + 1;
-        while (j < g.src.size() && g.src[j] == src + len && g.offs[j] == at + len) {
-            len += g.lens[j];
-            j++;
-        }
-        const hipError_t e = hipMemcpyAsync(dbuf + at, src, len, hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) {
-            return e;
-        }
-        k = j;
-    }
-    return hipSuccess;
-}
-
-double wall_s()
-{
-    struct timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
-    return (double) t.tv_sec + (double) t.tv_nsec * 1e-9;
-}
-
-// The single-device host batch on the calling thread's current device.
-// Sources are bufs[i] (host memory), or file ranges (fds[i], foffs[i]) when
-// fds is given.
-int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *foffs, const size_t *lens,
-                       const uint32_t *seeds, uint32_t *out_raw, size_t n)
-{
-    DeviceState *st;
-    if (device_state(&st) != CIO_OK) {
-        return CIO_ERROR;
-    }
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    // Groups of <= kStage bytes, 16-byte aligned segment placement.  The
-    // first groups are smaller (first_stage_bytes(), doubling up to kStage):
-    // the DMA engine starts after a short copy instead of a full slot's.
-    std::vector<HostGroup> groups(1);
-    uint64_t cap = std::min<uint64_t>(first_stage_bytes(), kStage);
-    for (size_t i = 0; i < n; i++) {
-        const uint8_t *p = fds ? nullptr : reinterpret_cast<const uint8_t *>(bufs[i]);
-        uint64_t left = lens[i], done = 0;
-        do {
-            HostGroup *g = &groups.back();
-            uint64_t at = (g->bytes + 15) & ~15ull;
-            if (at >= cap) {
-                groups.emplace_back();
-                g = &groups.back();
-                at = 0;
-                cap = std::min<uint64_t>(cap * 2, kStage);
-            }
-            const uint64_t take = std::min<uint64_t>(left, cap - at);
-            if (fds) {
-                g->fd.push_back(fds[i]);
-                g->foff.push_back(foffs[i] + done);
-            }
-            g->src.push_back(p ? p + done : nullptr);
-            g->offs.push_back(at);
-            g->lens.push_back(take);
-            g->cid.push_back((uint32_t) i);
-            g->bytes = at + take;
-            left -= take;
-            done += take;
-        } while (left > 0);
-    }
-
-    HostPipe *hp = nullptr;
-    hipError_t e = pipe_acquire(dev, &hp);
-    if (e != hipSuccess) {
-        return fail("cio_crc32_batch_host: device", e);
-    }
-    struct Release {
-        int dev;
-        HostPipe *hp;
-        ~Release() { pipe_release(dev, hp); }
-    } release{dev, hp};
-    if (!hp->ready && (e = pipe_init(*hp)) != hipSuccess) {
-        return fail("cio_crc32_batch_host: pipeline setup", e);
-    }
-    std::vector<uint32_t> init(n);
-    for (size_t i = 0; i < n; i++) {
-        init[i] = seeds ? seeds[i] : 0xffffffffu;
-    }
-    PipeSlot &s0 = hp->slot[0];
-    // Every slot is idle between calls (the previous call synchronised them).
-    e = grow_dev(&hp->state, &hp->state_cap, n, false, s0.stream);
-    if (e == hipSuccess) {
-        // Ordered before every kernel: group 0 runs on slot 0's stream after
-        // it, and each later group's kernel waits for the previous one's.
-        // (init outlives the call's final synchronisation.)
-        e = hipMemcpyAsync(hp->state, init.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s0.stream);
-    }
-    std::shared_lock<std::shared_mutex> rlk(g_reg_mu);
-    int rc = CIO_OK;
-    hipEvent_t prev = nullptr;
-    // CIO_GPU_PIPE_TIMING=1: per-call breakdown on stderr (diagnostic)
-    static const bool timing = getenv("CIO_GPU_PIPE_TIMING") != nullptr;
-    double t_copy = 0, t_wait = 0, t_plan = 0;
-    const double t_start = timing ? wall_s() : 0;
-    for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
-        PipeSlot &s = hp->slot[gi % kSlots];
-        const HostGroup &g = groups[gi];
-        const bool direct = group_registered(g);
-        double t = timing ? wall_s() : 0;
-        if (s.busy) {
-            // The slot's previous group (gi - kSlots) must be fully done.
-            if ((e = hipEventSynchronize(s.done)) != hipSuccess) break;
-            s.busy = false;
-        }
-        if (timing) {
-            t_wait += wall_s() - t;
-        }
-        cio_crc32_plan view;
-        uint32_t *d_cid = nullptr;
-        size_t meta_bytes = 0;
-        const char *err = nullptr;
-        // the group's plan (host image into the slot's pinned arena)
-        auto build = [&] {
-            const double tp = timing ? wall_s() : 0;
-            e = stage_plan(s, g, st, view, &d_cid, &meta_bytes, &err);
-            if (timing) {
-                t_plan += wall_s() - tp;
-            }
-        };
-        if (direct) {
-            build();
-        } else {
-            // staged: the plan is built while the copy workers fill the slot
-            const double tc = timing ? wall_s() : 0;
-            if (!hp->pool->copy(s.pinned, g, build)) {
-                rc = fail("cio_crc32_batch: short read from a file source");
-                break;
-            }
-            if (timing) {
-                t_copy += wall_s() - tc;
-            }
-        }
-        if (e != hipSuccess) break;
-        if (err) {
-            rc = fail(err);
-            break;
-        }
-        if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
-        if (direct) {
-            if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
-        } else {
-            if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
-        }
-        if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
-        if (plan_exec_impl(&view, s.dbuf, hp->state, hp->state, d_cid, s.stream) != CIO_OK) {
-            rc = CIO_ERROR;
-            break;
-        }
-        if ((e = hipEventRecord(s.done, s.stream)) != hipSuccess) break;
-        s.busy = true;
-        prev = s.done;
-    }
-    for (int b = 0; b < kSlots; b++) {
-        PipeSlot &s = hp->slot[b];
-        const hipError_t e2 = hipStreamSynchronize(s.stream);
-        if (e == hipSuccess) {
-            e = e2;
-        }
-        s.busy = false;
-    }
-    if (e == hipSuccess && rc == CIO_OK) {
-        e = hipMemcpy(out_raw, hp->state, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
-    }
-    if (timing) {
-        uint64_t total = 0;
-        for (const auto &g : groups) {
-            total += g.bytes;
-        }
-        fprintf(stderr, "batch_host: dev %d, %zu chunks, %zu groups, %.1f MB: total %.2f ms, copy %.2f ms, "
-                        "slot waits %.2f ms, plans %.2f ms\n", dev, n, groups.size(), total / 1e6,
-                (wall_s() - t_start) * 1e3, t_copy * 1e3, t_wait * 1e3, t_plan * 1e3);
-    }
-    if (e != hipSuccess) {
-        return fail("cio_crc32_batch_host", e);
-    }
-    return rc;
-}
-
-// Runs fn with `dev` as the calling thread's current device and restores the
-// previous one afterwards.
-template <typename F>
-int on_device(int dev, F fn)
-{
-    int prev = 0;
-    HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
-    if (prev != dev) {
-        HIP_TRY(hipSetDevice(dev), "hipSetDevice");
-    }
-    const int rc = fn();
-    if (prev != dev) {
-        (void) hipSetDevice(prev);
-    }
-    return rc;
-}
-
-}  // namespace
-
-extern "C" int cio_crc32_host_register(const void *p, size_t len)
-{
-    if (!p || len == 0) {
-        return fail("cio_crc32_host_register: empty range");
-    }
-    DeviceState *st;
-    if (device_state(&st) != CIO_OK) {
-        return CIO_ERROR;
-    }
-    std::unique_lock<std::shared_mutex> lk(g_reg_mu);
-    for (const auto &r : g_reg) {
-        if (r.first == reinterpret_cast<uintptr_t>(p)) {
-            return fail("cio_crc32_host_register: already registered");
-        }
-    }
-    // Portable: the pinned range is DMA-able by every device of the process,
-    // so multi-device batches take the direct path for it too.
-    const hipError_t e = hipHostRegister(const_cast<void *>(p), len, hipHostRegisterPortable);
-    if (e != hipSuccess) {
-        return fail("cio_crc32_host_register", e);
-    }
-    g_reg.emplace_back(reinterpret_cast<uintptr_t>(p), len);
-    return CIO_OK;
-}
-
-extern "C" int cio_crc32_host_unregister(const void *p)
-{
-    std::unique_lock<std::shared_mutex> lk(g_reg_mu);
-    for (size_t i = 0; i < g_reg.size(); i++) {
-        if (g_reg[i].first == reinterpret_cast<uintptr_t>(p)) {
-            const hipError_t e = hipHostUnregister(const_cast<void *>(p));
-            g_reg.erase(g_reg.begin() + (long) i);
-            return e == hipSuccess ? CIO_OK : fail("cio_crc32_host_unregister", e);
-        }
-    }
-    return fail("cio_crc32_host_unregister: not registered");
-}
-
-extern "C" int cio_crc32_batch_host(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
-                                    uint32_t *out_raw, size_t n)
-{
-    if (n == 0) {
-        return CIO_OK;
-    }
-    if (!bufs || !lens || !out_raw) {
-        return fail("cio_crc32_batch_host: null argument");
-    }
-    if (n >= 0xffffffffull) {
-        return fail("cio_crc32_batch_host: too many chunks");
-    }
-    return batch_host_current(bufs, nullptr, nullptr, lens, seeds, out_raw, n);
-}
-
-namespace {
-
-// Chunk i -> devices[i % G]: one host thread per device entry, each with its
-// own pipeline, stream and device buffers; no collective, results are
-// scattered back by chunk index.
-int batch_multi(const void *const *bufs, const int *fds, const uint64_t *foffs, const size_t *lens,
-                const uint32_t *seeds, uint32_t *out_raw, size_t n, const int *devices, int ndev,
-                const char *what)
-{
-    if (ndev <= 0) {
-        return batch_host_current(bufs, fds, foffs, lens, seeds, out_raw, n);
-    }
-    int visible = 0;
-    HIP_TRY(hipGetDeviceCount(&visible), "hipGetDeviceCount");
-    for (int d = 0; d < ndev; d++) {
-        if (devices[d] < 0 || devices[d] >= visible || devices[d] >= kMaxDev) {
-            return cioa_fail_msg(what, "device ordinal out of range");
-        }
-    }
-    const int G = (int) std::min<size_t>((size_t) ndev, n);
-    if (G == 1) {
-        return on_device(devices[0], [&] {
-            return batch_host_current(bufs, fds, foffs, lens, seeds, out_raw, n);
-        });
-    }
-    std::vector<int> rcs(G, CIO_OK);
-    std::vector<std::string> errs(G);
-    std::vector<std::thread> th;
-    th.reserve(G);
-    for (int d = 0; d < G; d++) {
-        th.emplace_back([&, d]() {
-            std::vector<const void *> b;
-            std::vector<int> f;
-            std::vector<uint64_t> fo;
-            std::vector<size_t> l;
-            std::vector<uint32_t> sd, o;
-            for (size_t i = (size_t) d; i < n; i += (size_t) G) {
-                if (fds) {
-                    f.push_back(fds[i]);
-                    fo.push_back(foffs[i]);
-                } else {
-                    b.push_back(bufs[i]);
-                }
-                l.push_back(lens[i]);
-                if (seeds) {
-                    sd.push_back(seeds[i]);
-                }
-            }
-            o.resize(l.size());
-            if (hipSetDevice(devices[d]) != hipSuccess) {
-                rcs[d] = CIO_ERROR;
-                errs[d] = "hipSetDevice";
-                return;
-            }
-            rcs[d] = batch_host_current(fds ? nullptr : b.data(), fds ? f.data() : nullptr,
-                                        fds ? fo.data() : nullptr, l.data(), seeds ? sd.data() : nullptr,
-                                        o.data(), l.size());
-            if (rcs[d] != CIO_OK) {
-                errs[d] = g_err;
-                return;
-            }
-            size_t k = 0;
-            for (size_t i = (size_t) d; i < n; i += (size_t) G) {
-                out_raw[i] = o[k++];
-            }
-        });
-    }
-    for (auto &t : th) {
-        t.join();
-    }
-    for (int d = 0; d < G; d++) {
-        if (rcs[d] != CIO_OK) {
-            char msg[96];
-            snprintf(msg, sizeof(msg), "%s: device %d", what, devices[d]);
-            return cioa_fail_msg(msg, errs[d].c_str());
-        }
-    }
-    return CIO_OK;
-}
-
-}  // namespace
-
-extern "C" int cio_crc32_batch_fd_multi(const int *fds, const uint64_t *foffs, const size_t *lens,
-                                        const uint32_t *seeds, uint32_t *out_raw, size_t n,
-                                        const int *devices, int ndev)
-{
-    if (n == 0) {
-        return CIO_OK;
-    }
-    if (!fds || !foffs || !lens || !out_raw || (ndev > 0 && !devices)) {
-        return fail("cio_crc32_batch_fd_multi: null argument");
-    }
-    if (n >= 0xffffffffull) {
-        return fail("cio_crc32_batch_fd_multi: too many chunks");
-    }
-    return batch_multi(nullptr, fds, foffs, lens, seeds, out_raw, n, devices, ndev, "cio_crc32_batch_fd_multi");
-}
-
-extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
-                                          uint32_t *out_raw, size_t n, const int *devices, int ndev)
-{
-    if (n == 0) {
-        return CIO_OK;
-    }
-    if (!bufs || !lens || !out_raw || (ndev > 0 && !devices)) {
-        return fail("cio_crc32_batch_host_multi: null argument");
-    }
-    if (n >= 0xffffffffull) {
-        return fail("cio_crc32_batch_host_multi: too many chunks");
-    }
-    return batch_multi(bufs, nullptr, nullptr, lens, seeds, out_raw, n, devices, ndev,
-                       "cio_crc32_batch_host_multi");
-}
-
-extern "C" int cio_gpu_device_count(void)
-{
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) {
-        return 0;
-    }
-    return n;
-}
-
-extern "C" int cio_gpu_set_device(int dev)
-{
-    HIP_TRY(hipSetDevice(dev), "hipSetDevice");
-    return CIO_OK;
-}
-
-extern "C" int cio_gpu_get_device(void)
-{
-    int dev = -1;
-    if (hipGetDevice(&dev) != hipSuccess) {
-        return -1;
-    }
-    return dev;
-}
