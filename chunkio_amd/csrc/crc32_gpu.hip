@@ -1043,8 +1043,10 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
                     st ^= r.q[q].x ^ r.q[q].y ^ r.q[q].z ^ r.q[q].w;
                 }
             } else {
+                // (the chain starts at 0: its first block needs no jump)
+                st = block16(lds, lb_lo, lb_hi, 0u, r.q[0]);
 #pragma unroll
-                for (int q = 0; q < kSub; ++q) {
+                for (int q = 1; q < kSub; ++q) {
                     st = shift_block16(lds, lb_lo, lb_hi, lrep, st, r.q[q]);
                 }
             }
