@@ -1347,7 +1347,9 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v5 gfx950 fused-stream ring1 uniform-desc xor3 prio-rotate coalesced-nt 4x16B-subchains slice4-lds32x perm horner-fold direct-whole small-chunk-kernel";
+    return "chunkio_amd crc32 v6 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains "
+           "slice4-lds32x perm horner-fold direct-whole) small(dpp-reduce bitop3-fold) "
+           "host(nt-staging graduated-groups pread-bounce multi-device)";
 }
 
 int cio_gpu_init(void)
