@@ -40,13 +40,16 @@ __attribute__((target("avx2"))) static void copy_nt_avx2(uint8_t *dst, const uin
 
 static int nt_enabled(void)
 {
+    /* Decided once; concurrent first callers compute the same value. */
     static int v = -1;
-    if (v < 0) {
+    int x = __atomic_load_n(&v, __ATOMIC_RELAXED);
+    if (x < 0) {
         const char *r = getenv("CIO_GPU_NT_COPY");
         __builtin_cpu_init();
-        v = (r == NULL || atoi(r) != 0) && __builtin_cpu_supports("avx2");
+        x = (r == NULL || atoi(r) != 0) && __builtin_cpu_supports("avx2");
+        __atomic_store_n(&v, x, __ATOMIC_RELAXED);
     }
-    return v;
+    return x;
 }
 
 __attribute__((visibility("hidden"))) int cioa_stage_nt(void)
