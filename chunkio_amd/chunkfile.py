@@ -83,6 +83,7 @@ def _bind():
         "cioa_stream_chunks": (S, [V, ctypes.POINTER(V), S]),
         "cioa_stream_size_chunks_up": (S, [V]),
         "cioa_scan_stream": (V, [V, ctypes.c_char_p, ctypes.c_char_p]),
+        "cioa_scan_dump": (I, [V, V]),
         "cioa_chunk_open": (V, [V, V, ctypes.c_char_p, I, S, IP]),
         "cioa_chunk_close": (None, [V, I]),
         "cioa_chunk_write": (I, [V, V, S]),
@@ -171,6 +172,26 @@ class Context:
             raise OSError(f"cannot scan stream {stream!r}")
         st = Stream(self, h, stream)
         return st, st.chunks()
+
+    def dump(self):
+        """The `tools/cio -l` listing of every stream (cioa_scan_dump), as text."""
+        import tempfile
+        libc = ctypes.CDLL(None)
+        libc.fopen.restype = ctypes.c_void_p
+        libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        libc.fclose.argtypes = [ctypes.c_void_p]
+        with tempfile.NamedTemporaryFile(prefix="cioa-dump-") as tf:
+            fp = libc.fopen(tf.name.encode(), b"w")
+            if not fp:
+                raise OSError("fopen failed")
+            try:
+                rc = self._lib.cioa_scan_dump(self._h, fp)
+            finally:
+                libc.fclose(fp)
+            if rc != 0:
+                raise OSError("cioa_scan_dump failed")
+            with open(tf.name, "r") as f:
+                return f.read()
 
     @property
     def last_chunk_error(self):

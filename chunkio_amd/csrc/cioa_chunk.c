@@ -608,8 +608,13 @@ cioa_stream *cioa_stream_create(cioa_ctx *ctx, const char *name)
     }
     st->name = strdup(name);
     st->ctx = ctx;
-    st->next = ctx->streams;
-    ctx->streams = st;
+    /* appended, creation order (mk_list_add, cio_stream.c:174): the listing
+     * walks streams in this order */
+    cioa_stream **tail = &ctx->streams;
+    while (*tail) {
+        tail = &(*tail)->next;
+    }
+    *tail = st;
     return st;
 }
 
@@ -1424,6 +1429,114 @@ cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext
 }
 
 /* ---- benchmark driver (tools/cio.c:367-466) ------------------------------- */
+
+/* ---- listing (tools/cio -l) --------------------------------------------- */
+
+/* One group of a stream's dump: recompute (one GPU batch) and print. */
+static void dump_flush(cioa_ctx *ctx, FILE *out, cioa_chunk **ch, int *set_down, size_t m)
+{
+    if (m == 0) {
+        return;
+    }
+    const void **bufs = malloc(m * sizeof(*bufs));
+    size_t *lens = malloc(m * sizeof(*lens));
+    uint32_t *seeds = malloc(m * sizeof(*seeds));
+    uint32_t *raw = malloc(m * sizeof(*raw));
+    int have = 0;
+    if (bufs && lens && seeds && raw && (ctx->flags & CIO_CHECKSUM)) {
+        for (size_t k = 0; k < m; k++) {
+            cioa_chunk *c = ch[k];
+            if (c->fs_size == 0) {
+                update_size(c);
+            }
+            const int64_t clen = cioa_st_content_len(c->map, c->fs_size, c->taint,
+                                                     (c->flags & CIO_OPEN_RW) != 0);
+            bufs[k] = c->map + CIOA_HDR_CONTENT_OFFSET;
+            lens[k] = 2 + (size_t) cioa_st_meta_len(c->map) + (clen > 0 ? (size_t) clen : 0);
+            seeds[k] = c->crc_cur;
+        }
+        have = cio_crc32_batch_host_multi(bufs, lens, seeds, raw, m, ctx->devs, ctx->ndev) == CIO_OK;
+    }
+    for (size_t k = 0; k < m; k++) {
+        cioa_chunk *c = ch[k];
+        char tmp[4096];
+        snprintf(tmp, sizeof(tmp) - 1, "%s/%s", c->st->name, c->name);
+        uint32_t be;
+        memcpy(&be, c->map + 2, sizeof(be));
+        const uint32_t crc_fs = ntohl(be);
+        fprintf(out, "        %-60s", tmp);
+        if (have) {
+            const uint32_t crc = raw[k] ^ 0xffffffffu;
+            if (crc != crc_fs) {
+                fprintf(out, "checksum error=%08x expected=%08x, ", crc_fs, crc);
+            }
+        }
+        fprintf(out, "meta_len=%d, data_size=%zu, crc=%08x\n", cioa_st_meta_len(c->map), c->data_size, crc_fs);
+        if (set_down[k]) {
+            cioa_chunk_down(c);
+        }
+    }
+    free(bufs);
+    free(lens);
+    free(seeds);
+    free(raw);
+}
+
+int cioa_scan_dump(cioa_ctx *ctx, FILE *out)
+{
+    if (!ctx || !out) {
+        return CIO_ERROR;
+    }
+    for (cioa_stream *st = ctx->streams; st; st = st->next) {
+        size_t n = 0;
+        for (cioa_chunk *c = st->head; c; c = c->next) {
+            n++;
+        }
+        fprintf(out, " stream:%-60s%i chunks\n", st->name, (int) n);
+        cioa_chunk **grp = malloc((n ? n : 1) * sizeof(*grp));
+        int *set_down = malloc((n ? n : 1) * sizeof(*set_down));
+        if (!grp || !set_down) {
+            free(grp);
+            free(set_down);
+            return CIO_ERROR;
+        }
+        size_t m = 0, downs = 0;
+        for (cioa_chunk *c = st->head; c; c = c->next) {
+            int sd = 0;
+            if (!cioa_chunk_is_up(c)) {
+                int ret = cioa_chunk_up(c);
+                if (ret == CIO_ERROR && downs > 0 && ctx->total_up >= ctx->max_up) {
+                    /* the chunks this dump brought up hold the budget: print
+                     * and release them, as the reference's one-at-a-time
+                     * loop would have, then retry */
+                    dump_flush(ctx, out, grp, set_down, m);
+                    m = downs = 0;
+                    ret = cioa_chunk_up(c);
+                }
+                if (ret != CIO_OK) {
+                    continue;                       /* cio_file.c:1334-1336 */
+                }
+                sd = 1;
+                downs++;
+            }
+            if (catch_up(c) != CIO_OK) {            /* deferred: crc_cur and map+2 as the reference has them */
+                if (sd) {
+                    cioa_chunk_down(c);
+                    downs--;
+                }
+                continue;
+            }
+            grp[m] = c;
+            set_down[m] = sd;
+            m++;
+        }
+        dump_flush(ctx, out, grp, set_down, m);
+        free(grp);
+        free(set_down);
+    }
+    return CIO_OK;
+}
+
 
 int cioa_bench_perf_write(const char *root, const void *data, size_t len, int files, int writes,
                           int batch, int flags, double *secs, uint64_t *bytes)

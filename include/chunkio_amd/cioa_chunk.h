@@ -24,6 +24,7 @@
  *   cioa_chunk_tx_begin / _commit / _rollback          src/cio_chunk.c:423-502
  *   cioa_chunk_is_up / _up / _up_force / _down         src/cio_chunk.c:509-605, cio_file.c:816-959
  *   cioa_meta_write / _read / _cmp / _size             src/cio_meta.c:46-180, cio_file.c:1075-1145
+ *   cioa_scan_dump                      src/cio_scan.c:171-190, cio_file.c:1316-1375 (tools/cio -l)
  *   cioa_scan_stream                    src/cio_scan.c:39-125 (verify-on-load of a stream
  *                                       directory, CIO_DELETE_IRRECOVERABLE :107-118)
  *
@@ -50,6 +51,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <sys/types.h>
 
 #ifdef __cplusplus
@@ -127,6 +129,18 @@ size_t cioa_stream_chunks(cioa_stream *st, cioa_chunk **out, size_t cap);
  * the failure was BAD_CHECKSUM / BAD_FILE_SIZE / BAD_LAYOUT.  Returns the
  * stream (created if needed) or NULL. */
 cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *chunk_extension);
+
+/* The listing of `tools/cio -l` (cio_scan_dump, src/cio_scan.c:171-190 ->
+ * cio_file_scan_dump, src/cio_file.c:1316-1375), same text, to out: per stream
+ * " stream:%-60s%i chunks", per chunk "        %-60s" then, with CIO_CHECKSUM and a
+ * mismatch, "checksum error=%08x expected=%08x, " (header value first, as the
+ * reference prints them), then "meta_len=%d, data_size=%zu, crc=%08x".  Down
+ * chunks are brought up for it and down again; one that cannot come up is left
+ * out.  The recompute is the reference's: crc_update(crc_cur, region) --
+ * seeded from crc_cur, not crc_init(), so a chunk loaded with a verified
+ * crc_cur lists as a checksum error, as it does in the reference.
+ * A stream's recomputes run as one GPU batch. */
+int cioa_scan_dump(cioa_ctx *ctx, FILE *out);
 
 /* ---- chunks ------------------------------------------------------------- */
 

@@ -425,3 +425,87 @@ def test_scan_stream_delete_irrecoverable(cuda, tmp_path):
     assert [c.data_size for c in chunks] == [1000 * i + 1 for i in range(20) if i != 5]
     ctx.close()
     assert not (tmp_path / "s" / "c05").exists()
+
+
+def _expected_dump(root, streams, checksum):
+    """cio_scan_dump / cio_file_scan_dump (src/cio_scan.c:171-190,
+    src/cio_file.c:1316-1375) restated over the chunks' bytes: streams =
+    [(name, [(chunk name, map bytes, crc_cur, data_size)])] as the dump sees them
+    (a down chunk after its verify on up: crc_cur = CRC of its region)."""
+    out = []
+    for sname, chunks in streams:
+        out.append(" stream:%-60s%i chunks\n" % (sname, len(chunks)))
+        for cname, m, crc_cur, data_size in chunks:
+            meta_len = struct.unpack(">H", m[22:24])[0]
+            clen = struct.unpack(">I", m[10:14])[0]
+            crc_fs = struct.unpack(">I", m[2:6])[0]
+            line = "        %-60s" % f"{sname}/{cname}"
+            if checksum:
+                crc = po.crc_update(crc_cur, m[22:24 + meta_len + clen]) ^ INIT
+                if crc != crc_fs:
+                    line += "checksum error=%08x expected=%08x, " % (crc_fs, crc)
+            line += "meta_len=%d, data_size=%d, crc=%08x\n" % (meta_len, data_size, crc_fs)
+            out.append(line)
+    return "".join(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [cf.CIO_CHECKSUM, 0, cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC])
+def test_scan_dump_listing(cuda, tmp_path, data400, flags):
+    # tools/cio -l: a synced chunk with metadata, an unsynced one, a down one,
+    # and a chunk loaded by a stream scan (its crc_cur is the verified CRC, so
+    # the reference's dump reports it as a checksum error: SURVEY a15).
+    root = str(tmp_path / "root")
+    with cf.Context(root, flags=flags) as ctx:
+        st = ctx.stream("s1")
+        a, _ = st.open("a.flb")
+        a.meta_write(b"tag-a")
+        a.write(data400[:5000])
+        a.sync()
+        b, _ = st.open("b.flb")
+        b.write(b"unsynced bytes")
+        d, _ = st.open("d.flb")
+        d.write(data400[:777])
+        d.sync()
+        d.down()
+        st2 = ctx.stream("s2")
+        e, _ = st2.open("e.flb")
+        e.write(b"x" * 100)
+        e.sync()
+        e.close()
+    with cf.Context(root, flags=flags) as ctx:
+        st1, _ = ctx.scan("s1")
+        st2, _ = ctx.scan("s2")
+        chunks = {c.name: c for c in st1.chunks()}
+        b = chunks["b.flb"]
+        b.write(b" more")                                        # unsynced again, after the load
+        assert chunks["d.flb"].down() == cf.CIO_OK                # listed through up + down
+        views = []
+        for sname, stream in (("s1", st1), ("s2", st2)):
+            ent = []
+            for c in stream.chunks():
+                if not c.is_up():
+                    with open(os.path.join(root, sname, c.name), "rb") as f:
+                        m = f.read()
+                    meta_len = struct.unpack(">H", m[22:24])[0]
+                    clen = struct.unpack(">I", m[10:14])[0]
+                    crc_cur = po.crc_update(INIT, m[22:24 + meta_len + clen]) if flags & cf.CIO_CHECKSUM else INIT
+                    ent.append((c.name, m, crc_cur, clen))
+                else:
+                    if flags & cf.CIOA_DEFERRED_CRC:
+                        ent.append((c.name, None, None, c.data_size))   # filled after the dump
+                    else:
+                        ent.append((c.name, bytes(c.map), c.crc_cur, c.data_size))
+            views.append((sname, ent))
+        text = ctx.dump()
+        if flags & cf.CIOA_DEFERRED_CRC:
+            # the dump brings a deferred chunk's crc_cur and raw header up to
+            # date first (as the reference's per-write path has them)
+            for sname, ent in views:
+                for k, (name, m, crc_cur, ds) in enumerate(ent):
+                    if m is None:
+                        c = {c.name: c for c in (st1 if sname == "s1" else st2).chunks()}[name]
+                        ent[k] = (name, bytes(c.map), c.crc_cur, ds)
+        want = _expected_dump(root, views, flags & cf.CIO_CHECKSUM)
+        assert text == want, (text, want)
+        assert "d.flb" in text and "unsynced" not in text
