@@ -78,13 +78,14 @@ int cio_file_verify_batch(cio_verify_item *items, size_t n, int flags);
 int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags,
                                 const int *devices, int ndev);
 
-/* Open + mmap (read-only unless CIOA_VERIFY_WRITEBACK) + verify n chunk files,
- * the batched equivalent of loading a stream directory
+/* Open (read-only unless CIOA_VERIFY_WRITEBACK) + verify n chunk files, the
+ * batched equivalent of loading a stream directory
  * (cio_scan_stream_files, src/cio_scan.c:39-125).  status[i], error[i],
  * crc_raw[i] per file; a file that cannot be opened, stat'ed or read gets
  * CIO_ERROR.  The files are not mapped: headers are read with pread() on up
  * to 16 host threads, and the CRC regions stream from the files into the GPU
- * pipeline (cio_crc32_batch_fd_multi).  With CIOA_VERIFY_WRITEBACK the files
+ * pipeline (cio_crc32_batch_fd_multi: pread through a per-thread bounce
+ * buffer, streaming stores into pinned staging).  With CIOA_VERIFY_WRITEBACK the files
  * are opened read-write (inferred legacy lengths written back, empty files
  * initialised).  With CIOA_VERIFY_DELETE_IRRECOVERABLE the irrecoverable
  * files are unlinked after the batch, as cio_scan does. */
