@@ -20,6 +20,14 @@ constexpr int kSub = 4;                     // sub-chains per lane
 constexpr int kRow = kWave * kGran;         // 1024: one coalesced wave-instruction
 constexpr int kStep = kSub * kRow;          // 4096 bytes per wave-step
 constexpr int kThreads = 1024;              // one workgroup per CU
+constexpr uint32_t kWavesPerWg = kThreads / kWave;   // 16
+// Per-wave flags (the plan's pfac array continues with one word per wave):
+//   bit 0: the wave's first chunk began in an earlier wave of this workgroup
+//          and ends in this wave's range (the wave folds it through LDS);
+//   bits 8..15: how many waves before this one hold its earlier pieces;
+//   bit 1: the range ends inside a chunk whose pieces all lie in this
+//          workgroup (the wave hands that piece over through LDS).
+constexpr uint32_t kWfFold = 1u, kWfPublish = 2u;
 constexpr int kX8Count = 2 * kStep;         // x^(8m), m in [0, 8192)
 constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
@@ -35,7 +43,8 @@ struct ChunkDesc {
     uint32_t nsteps;   // ceil(vlen / kStep); 0 for tiny chunks (len < 4)
     uint32_t h;        // off & 15 (zeroed head bytes)
     uint32_t npieces;  // waves holding a piece of this chunk
-    uint32_t pad[3];
+    uint32_t w0, w1;   // first and last wave holding a piece (npieces > 0)
+    uint32_t pad;
 };
 static_assert(sizeof(ChunkDesc) == 48, "desc layout");
 
@@ -63,7 +72,7 @@ struct PlanHost {
     std::vector<ChunkDesc> desc;
     std::vector<WaveStart> ws;
     std::vector<uint32_t> tiny;
-    std::vector<uint32_t> pfac;   // per piece slot (wave + chunk)
+    std::vector<uint32_t> pfac;   // per piece slot (wave + chunk), then W wave flags, then W last-piece factors
     uint64_t S = 0, bytes = 0;
 };
 

@@ -103,27 +103,37 @@ struct MulCols {
     }
 };
 
+// One v_bfe_i32 (the bit as a 0 / ~0 mask) and one v_bitop3_b32 (x ^ (m & c))
+// per bit into four accumulators: 66 instructions without a loop-carried
+// shift, ~0.15 us for a wave alone against ~0.4 us for multmodp
+// (tools/probe/gf2_probe.hip) -- the fold at a wave's range end runs while
+// the rest of the CU may be idle.
 template <uint32_t C>
 __device__ __forceinline__ uint32_t mulconst(uint32_t b)
 {
     constexpr MulCols<C> K;
-    uint32_t p = 0;
+    uint32_t p[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
-        p ^= K.v[j] & (0u - ((b >> j) & 1u));
+        p[j & 3] = __builtin_amdgcn_bitop3_b32(p[j & 3], 0u - ((b >> j) & 1u), K.v[j], 0x78);
     }
-    return p;
+    return __builtin_amdgcn_bitop3_b32(p[0], p[1], p[2], 0x96) ^ p[3];
 }
 
 // Sub-chain states of a lane whose last step was full, shifted to the lane's
-// row end and XORed: sum_q s_q x^(8 * 1024 (3 - q)), by Horner.
+// row end and XORed: sum_q s_q x^(8 * 1024 (3 - q)), by Horner.  TREE: the
+// bit-column form (fewer instructions in a row: uniform batches end all their
+// pieces together at the kernel's end, where one wave's latency counts); the
+// shift-chain form measured 0.2% faster where pieces end mid-stream among
+// streaming waves (cfg3, profiles/r02/ab_lds_fold_preshifted.txt).
+template <bool TREE>
 __device__ __forceinline__ uint32_t fold_full(const uint32_t (&s)[kSub])
 {
     constexpr uint32_t kXRow = cx_xpow8n(kRow);
     uint32_t h = s[0];
 #pragma unroll
     for (int q = 1; q < kSub; ++q) {
-        h = multmodp(kXRow, h) ^ s[q];
+        h = (TREE ? mulconst<kXRow>(h) : multmodp(kXRow, h)) ^ s[q];
     }
     return h;
 }
@@ -157,11 +167,6 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
 __device__ __forceinline__ uint64_t wave_start(uint64_t w, uint64_t S, uint64_t W)
 {
     return div_u52(w * S, W);
-}
-
-__device__ __forceinline__ uint64_t wave_of_step(uint64_t g, uint64_t S, uint64_t W)
-{
-    return div_u52((g + 1) * W + S - 1, S) - 1;
 }
 
 // Slice tables in LDS, replicated 32x so lane l always reads bank (l & 31):
@@ -431,6 +436,14 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
                        __builtin_amdgcn_readlane((int) v, 32) ^ __builtin_amdgcn_readlane((int) v, 48));
 }
 
+// A relaxed load at workgroup scope: a VECTOR load even for a uniform
+// address (an outstanding scalar load would force lgkmcnt(0) on every LDS
+// lookup of the CRC), counted in vmcnt with the ring's data loads.
+__device__ __forceinline__ uint32_t load_vec_u32(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // x ^ (m & c) as one v_bitop3_b32 (truth table 0x78 over x, m, c).
 __device__ __forceinline__ uint32_t xor_and(uint32_t x, uint32_t m, uint32_t c)
 {
@@ -440,23 +453,22 @@ __device__ __forceinline__ uint32_t xor_and(uint32_t x, uint32_t m, uint32_t c)
 }
 
 // All pieces of chunk c folded into one raw CRC by the last wave to publish
-// one: XOR over pieces of shift(piece, bytes after it), lanes in parallel.
-// The shift factors x^(8 * bytes after the piece) are per piece slot and
-// precomputed by the plan, so a fold is one round of independent loads.
-__device__ __forceinline__ void fold_chunk(uint64_t g, uint32_t nsteps, uint32_t c, uint32_t oc,
+// one: every partial is already shifted to the chunk end (a non-final piece
+// by its wave's factor F, the final piece needs none), so the fold is one
+// round of independent loads and an XOR, lanes in parallel.
+__device__ __forceinline__ void fold_chunk(uint32_t w0, uint32_t w1, uint32_t c, uint32_t oc,
                                            uint32_t lane, const unsigned long long *partials,
-                                           const uint32_t *pfac, uint32_t *out, uint32_t *counters,
-                                           uint64_t S, uint32_t W)
+                                           const uint32_t *pfac, uint32_t *out, uint32_t *counters)
 {
-    const uint64_t w0 = wave_of_step(g, S, W);
-    const uint64_t w1 = wave_of_step(g + nsteps - 1, S, W);
+    // Waves w0..w1 (the plan's) hold the pieces; a wave with an empty range
+    // in between has fold factor 0 in its slot, and its stale slot is skipped.
     uint32_t acc = 0;
-    for (uint64_t wb = w0; wb <= w1; wb += kWave) {
-        const uint64_t wv = wb + lane;
-        if (wv <= w1 && wave_start(wv, S, W) < wave_start(wv + 1, S, W)) {
+    for (uint32_t wb = w0; wb <= w1; wb += kWave) {
+        const uint32_t wv = wb + lane;
+        if (wv <= w1) {
             const uint32_t p = (uint32_t) __hip_atomic_load(&partials[wv + c], __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
-            acc ^= multmodp(pfac[wv + c], p);
+            acc ^= pfac[wv + c] ? p : 0u;
         }
     }
     acc = wave_xor(acc);
@@ -514,6 +526,16 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 // access.  The general path reads its WaveStart record first.  Separate
 // instantiations keep the general path's scalar-load wait out of the
 // uniform one's prologue.
+// Diagnostic builds only (make ablib DEFS=...): skip the arrival/fold step
+// (outputs of split chunks are then wrong) to price the kernel's tail.
+#ifndef CIO_DIAG_NO_ARRIVAL
+#define CIO_DIAG_NO_ARRIVAL 0
+#endif
+// Chunks whose pieces all lie in one workgroup are folded through LDS after
+// the stream (A/B knob: 0 = every split chunk takes the global arrival).
+#ifndef CIO_LDS_FOLD
+#define CIO_LDS_FOLD 1
+#endif
 template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
@@ -622,12 +644,14 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // arrival step at the end; fetched now so that they cost nothing there.
     // Clamped, not predicated: a branch would break the ring's vmcnt tracking.
     uint64_t ar_g;
-    uint32_t ar_ns, ar_np;
+    uint32_t ar_ns, ar_np, ar_w0, ar_w1;
     {
         const ChunkDesc &ad = desc[min(c0 + lane, n - 1)];
         ar_g = ad.g;
         ar_ns = ad.nsteps;
         ar_np = ad.npieces;
+        ar_w0 = ad.w0;
+        ar_w1 = ad.w1;
     }
     // Fold factor of a piece that ends with a full step (the common case):
     // sub-chain q of lane l then ends 1024 (3 - q) + 16 (63 - l) bytes before
@@ -635,6 +659,19 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // (fold_full); the lane part x^(8 * 16 (63 - l)) is fetched once here
     // instead of gathered from g_x8 at every piece end.
     const uint32_t xl = g_x8[kRow - (lane + 1) * kGran];
+    // Workgroup-local fold.  A split chunk whose pieces all lie in this
+    // workgroup's 16 waves skips the partial slot and the arrival counter:
+    // each non-final piece (a wave's last piece) goes to the wave's LDS word
+    // once the stream is over, and the wave holding the final piece (its
+    // first chunk c0, begun before its range) folds them there.  Its fold
+    // factors are fetched now, so the fold at the end waits on no HBM access.
+    // The plan's per-wave words follow the piece slots: the LDS-fold flags
+    // (kWfFold, kWfPublish) and the fold factor of the wave's last piece
+    // (x^(8 * chunk bytes after it); 1 when that piece ends its chunk).
+    const uint32_t *wwords = pfac + (W + n + 1);
+    const uint32_t wfl = CIO_LDS_FOLD ? load_vec_u32(wwords + wave) : 0u;
+    const uint32_t wlast = load_vec_u32(wwords + W + wave);
+    uint32_t fold_own = 0, pub = 0;
     // Keep the scheduler from sinking these loads below the table build (and
     // the table arithmetic from rising above them: the first step's HBM
     // requests leave before any table work).
@@ -660,6 +697,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     if (active) {
         uint32_t s[kSub] = {0u, 0u, 0u, 0u};
         uint64_t e[kSub] = {0ull, 0ull, 0ull, 0ull};
+        uint32_t xlast = 0;    // F, below
         uint32_t full_end = (uint32_t) (d.vlen / kStep);
         uint32_t seed = (j == 0) ? (seeds ? seeds[cid ? cid[c] : c] : 0xffffffffu) : 0u;
         uint64_t g = g0;
@@ -710,9 +748,11 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         // with the constant x^(8 * 1024), then the lane factor.
                         // (The asm keeps the compiler from hoisting xl's 32
                         // bit masks out of the loop into 64 spilled SGPRs.)
-                        uint32_t a = xl;
+                        // A non-final piece (the range's last) takes F instead
+                        // of the lane factor, landing at the chunk end.
+                        uint32_t a = j < d.nsteps ? xlast : xl;
                         asm volatile("" : "+v"(a));
-                        contrib = multmodp(a, fold_full(s));
+                        contrib = multmodp(a, fold_full<UNIFORM>(s));
                     } else {
                         const uint64_t pend = min(j * kStep, d.vlen);
                         contrib = 0;
@@ -729,6 +769,10 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         if (lane == 0) {
                             out[cid ? cid[c] : c] = contrib;
                         }
+                    } else if (j == d.nsteps && (wfl & kWfFold)) {
+                        fold_own = contrib;    // the final piece of c0 (== c)
+                    } else if (j < d.nsteps && (wfl & kWfPublish)) {
+                        pub = contrib;         // the range ends inside a local chunk
                     } else {
                         __hip_atomic_store(&partials[(uint64_t) wave + c], (unsigned long long) contrib,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -764,9 +808,17 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             t_first = __builtin_amdgcn_s_memrealtime();
         }
         const uint64_t iters = gend - g0;
+        // F = x^(8 * 16 (63 - l)) * wlast, the full fold factor of the last
+        // piece per lane, so that a non-final piece lands in its slot already
+        // shifted to the chunk end and no fold multiplies.  Computed in the
+        // second iteration (the first if there is one), off the start-up path.
+        const uint64_t it_f = iters > 1 ? 1 : 0;
         for (uint64_t it = 0; it < iters; ++it) {
             if (PRIO) {
                 rotate_prio(slot_group, it);
+            }
+            if (it == it_f) {
+                xlast = multmodp(xl, wlast);
             }
             const bool pe = crc_step(cur);
             if (STAMPS && it == 0) {
@@ -798,11 +850,14 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // chunks were written out directly); the batch of 64 ends the scan
         // if it reaches a non-empty chunk that starts past the range (or the
         // end of the batch).
-        for (uint32_t ac = c0;;) {
+        for (uint32_t ac = c0; !CIO_DIAG_NO_ARRIVAL;) {
             const uint32_t idx = ac + lane;
             const bool inb = idx < n;
             const bool whole = ar_g >= g0 && ar_g + ar_ns <= gend;
-            const bool member = inb && ar_ns != 0 && ar_g < gend && !whole;
+            // Workgroup-local chunks (first and last piece in one workgroup)
+            // were folded through LDS.
+            const bool local = CIO_LDS_FOLD && (ar_w0 ^ ar_w1) < kWavesPerWg;
+            const bool member = inb && ar_ns != 0 && ar_g < gend && !whole && !local;
             const bool stop = !inb || (ar_ns != 0 && ar_g >= gend);
             uint32_t old = 0;
             if (member) {
@@ -811,10 +866,8 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             for (uint64_t fin = __ballot(member && old + 1 == ar_np); fin; fin &= fin - 1) {
                 const uint32_t b = (uint32_t) __builtin_ctzll(fin);
                 const uint32_t fc = ac + b;
-                const uint64_t fg = ((uint64_t) (uint32_t) __builtin_amdgcn_readlane((uint32_t) (ar_g >> 32), b) << 32) |
-                                    (uint32_t) __builtin_amdgcn_readlane((uint32_t) ar_g, b);
-                fold_chunk(fg, __builtin_amdgcn_readlane(ar_ns, b), fc, cid ? cid[fc] : fc, lane,
-                           partials, pfac, out, counters, S, W);
+                fold_chunk(__builtin_amdgcn_readlane(ar_w0, b), __builtin_amdgcn_readlane(ar_w1, b), fc,
+                           cid ? cid[fc] : fc, lane, partials, pfac, out, counters);
             }
             if (__ballot(stop)) {
                 break;
@@ -824,10 +877,44 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             ar_g = ad.g;
             ar_ns = ad.nsteps;
             ar_np = ad.npieces;
+            ar_w0 = ad.w0;
+            ar_w1 = ad.w1;
         }
     }
 
     tiny_chunks(lds, lb_lo, base, desc, tiny, seeds, out, cid, ntiny, wave, lane, W);
+    if (CIO_LDS_FOLD) {
+        // Every wave is past its last table lookup: the LDS words are free.
+        __syncthreads();
+        uint32_t *slot = reinterpret_cast<uint32_t *>(lds);
+        if (lane == 0) {
+            slot[tid >> 6] = pub;    // 0 unless the range ended inside a local chunk
+        }
+        __syncthreads();
+        if (wfl & kWfFold) {
+            // Lane i < 16 <-> wave (wave - 16 + i); the nb waves before this
+            // one hold the chunk's earlier pieces (empty ranges published 0).
+            const uint32_t nb = (wfl >> 8) & 0xffu;
+            uint32_t a = 0;
+            if (lane < kWavesPerWg && lane >= kWavesPerWg - nb) {
+                a = slot[(tid >> 6) + lane - kWavesPerWg];
+            }
+            a = wave_xor(a) ^ fold_own;
+            if (lane == 0) {
+                out[cid ? cid[c0] : c0] = a;
+            }
+        }
+    }
+#if defined(CIO_DIAG_TAIL) && CIO_DIAG_TAIL == 1
+    {   // diagnostic: finished waves stay resident ~5 us (sleeping) before exiting
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < 500) {
+            __builtin_amdgcn_s_sleep(10);
+        }
+    }
+#elif defined(CIO_DIAG_TAIL) && CIO_DIAG_TAIL == 2
+    __syncthreads();   // diagnostic: finished waves wait for the workgroup before exiting
+#endif
     if (STAMPS && lane == 0) {
         // Diagnostic build only: 100 MHz global clock, per wave.
         uint32_t hw_id, xcc_id;
@@ -882,13 +969,6 @@ struct SmallRegs {
     uint32_t seed;   // the chunk's seed
 };
 
-// A relaxed load at workgroup scope: a VECTOR load even for a uniform
-// address (an outstanding scalar load would force lgkmcnt(0) on every LDS
-// lookup of the CRC), counted in vmcnt with the ring's data loads.
-__device__ __forceinline__ uint32_t load_vec_u32(const uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // Zero the bytes of a 16-byte block at virtual offset bs past the end v.
 __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
@@ -1347,8 +1427,8 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v6 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains "
-           "slice4-lds32x perm horner-fold direct-whole) small(dpp-reduce bitop3-fold) "
+    return "chunkio_amd crc32 v7 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains "
+           "slice4-lds32x perm horner-fold direct-whole preshifted-partials wg-lds-fold) small(dpp-reduce bitop3-fold) "
            "host(nt-staging graduated-groups pread-bounce multi-device)";
 }
 
@@ -1448,8 +1528,9 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
         return m < x4k.size() ? cioa_multmodp(x4k[m], x8[r]) : cioa_xpow8n(d);
     };
 
-    std::vector<uint32_t> wc(W, 0);
-    ph.pfac.assign((size_t) W + n + 1, 0u);
+    std::vector<uint32_t> wc(W, 0), wl(W, 0);
+    const size_t nslots = (size_t) W + n + 1;
+    ph.pfac.assign(nslots + 2 * (size_t) W, 0u);
     if (S > 0) {
         size_t c = 0;
         for (uint32_t w = 0; w < W; w++) {
@@ -1465,6 +1546,11 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
             for (size_t k = c; k < n && ph.desc[k].g < g1; k++) {
                 ChunkDesc &d = ph.desc[k];
                 if (d.nsteps) {
+                    if (d.npieces == 0) {
+                        d.w0 = w;
+                    }
+                    d.w1 = w;
+                    wl[w] = (uint32_t) k;
                     d.npieces++;
                     const uint64_t pend = std::min(std::min(g1 - d.g, (uint64_t) d.nsteps) * (uint64_t) kStep,
                                                    d.vlen);
@@ -1472,6 +1558,30 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
                 }
             }
         }
+    }
+    // Workgroup-local chunks: split, with every piece in one workgroup.
+    auto local = [](const ChunkDesc &d) {
+        return d.npieces > 1 && d.w0 / kWavesPerWg == d.w1 / kWavesPerWg;
+    };
+    for (uint32_t w = 0; S > 0 && w < W; w++) {
+        const uint64_t g0 = ((uint64_t) w * S) / W;
+        const uint64_t g1 = ((uint64_t) (w + 1) * S) / W;
+        if (g0 == g1) {
+            continue;
+        }
+        uint32_t f = 0;
+        const ChunkDesc &first = ph.desc[wc[w]];
+        if (first.g < g0 && first.g + first.nsteps <= g1 && local(first)) {
+            f |= kWfFold | ((w - first.w0) << 8);
+        }
+        const ChunkDesc &last = ph.desc[wl[w]];
+        const bool nonfinal = last.g + last.nsteps > g1;
+        if (nonfinal && local(last)) {
+            f |= kWfPublish;
+        }
+        ph.pfac[nslots + w] = f;
+        // The last piece's factor (x^0 = 0x80000000 when it ends its chunk).
+        ph.pfac[nslots + W + w] = nonfinal ? ph.pfac[w + wl[w]] : 0x80000000u;
     }
     ph.ws.assign(W, WaveStart{});
     for (uint32_t w = 0; w < W; w++) {
@@ -1576,6 +1686,28 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     }
     *out = p;
     return CIO_OK;
+}
+
+/* Test hook (not in the public header; host only, no device): the plan's
+ * work split for W waves.  Per chunk: w0, w1, npieces (3 words); per wave:
+ * the LDS-fold flags.  Returns 0, or -1 on a plan error. */
+int cioa_debug_plan_layout(const uint64_t *offs, const uint64_t *lens, size_t n, uint32_t W,
+                           uint32_t *chunk_words, uint32_t *wave_flags)
+{
+    PlanHost ph;
+    if (plan_build(ph, offs, lens, n, W) != nullptr) {
+        return -1;
+    }
+    for (size_t i = 0; i < n; i++) {
+        chunk_words[3 * i + 0] = ph.desc[i].w0;
+        chunk_words[3 * i + 1] = ph.desc[i].w1;
+        chunk_words[3 * i + 2] = ph.desc[i].npieces;
+    }
+    const size_t nslots = (size_t) W + n + 1;
+    for (uint32_t w = 0; w < W; w++) {
+        wave_flags[w] = ph.pfac[nslots + w];
+    }
+    return 0;
 }
 
 /* Diagnostic (not in the public header): copy the per-wave timestamps of the

@@ -175,6 +175,27 @@ def test_small_chunk_fewer_chunks_than_waves(cuda):
         np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
 
 
+@pytest.mark.parametrize("kind", ["cross_workgroup", "mixed_local", "fewer_steps_than_waves"])
+def test_workgroup_local_and_cross_workgroup_pieces(cuda, kind):
+    """Split chunks whose pieces all lie in one 16-wave workgroup are folded
+    through LDS after the stream; the others take the global arrival.  These
+    batches put both kinds side by side (and, for the last, empty wave ranges
+    between a chunk's pieces), with seeds and head misalignment."""
+    rng = np.random.default_rng(len(kind))
+    if kind == "cross_workgroup":
+        lens = np.full(64, 409600, np.uint64)            # ~64 waves per chunk
+    elif kind == "mixed_local":
+        lens = rng.integers(90_000, 120_000, 1100).astype(np.uint64)   # ~4 waves per chunk
+    else:
+        lens = rng.integers(1, 40_000, 40).astype(np.uint64)
+    buf, offs = wl.host_batch(0x5EED + len(kind), lens)
+    offs = offs + rng.integers(0, 16, len(offs)).astype(np.uint64)
+    buf = np.concatenate([buf, np.zeros(32, np.uint8)])
+    seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+    np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds),
+                                  po.crc_batch(buf, offs, lens, seeds=seeds))
+
+
 def test_one_huge_chunk_spans_all_waves(cuda):
     n = 48 * 1024 * 1024 + 12345
     data = wl.gen_chunk(0xBEEF, 0, n)

@@ -128,3 +128,73 @@ def test_model_matches_crc_update(W):
     got = model(buf, offs, lens, seeds, W)
     want = [po.crc_update(s, buf[o:o + n]) for s, o, n in zip(seeds, offs, lens)]
     assert got == want
+
+
+def _layout(offs, lens, W):
+    import ctypes
+    from chunkio_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.cioa_debug_plan_layout
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    f.argtypes = [u64p, u64p, ctypes.c_size_t, ctypes.c_uint32, u32p, u32p]
+    o = np.ascontiguousarray(offs, np.uint64)
+    n_ = np.ascontiguousarray(lens, np.uint64)
+    cw = np.zeros(3 * len(o), np.uint32)
+    wf = np.zeros(W, np.uint32)
+    assert f(o.ctypes.data_as(u64p), n_.ctypes.data_as(u64p), len(o), W,
+             cw.ctypes.data_as(u32p), wf.ctypes.data_as(u32p)) == 0
+    return cw.reshape(-1, 3), wf
+
+
+@pytest.mark.parametrize("W,kind", [(4096, "cfg2"), (4096, "mixed"), (4096, "fewer_steps"), (256, "mixed")])
+def test_plan_workgroup_local_fold_flags(W, kind):
+    """The C plan's per-chunk wave range (w0, w1) and per-wave LDS-fold flags
+    (crc32_gpu.hip plan_build) against a restatement of their definition:
+    a split chunk whose first and last piece lie in one 16-wave workgroup is
+    folded by the wave holding its final piece (bit 0, bits 8.. = waves
+    before it), and every earlier wave ending inside it hands its piece over
+    (bit 1); all other split chunks take the global arrival."""
+    rng = np.random.default_rng(W + len(kind))
+    if kind == "cfg2":
+        lens = np.full(1024, 409600, np.uint64)
+    elif kind == "mixed":
+        lens = rng.integers(1, 3 << 20, 3000).astype(np.uint64)
+        lens[::7] = rng.integers(0, 4, lens[::7].size)
+    else:
+        lens = rng.integers(1, 40000, 40).astype(np.uint64)   # S < W: empty wave ranges
+    offs = np.cumsum(np.concatenate([[5], lens[:-1] + 3])).astype(np.uint64)
+    if kind == "cfg2":
+        offs = np.arange(1024, dtype=np.uint64) * np.uint64(409600)
+    desc, S, wc = plan(list(map(int, offs)), list(map(int, lens)), W)
+    cw, wf = _layout(offs, lens, W)
+    start = lambda w: (w * S) // W  # noqa: E731
+    wave_of = lambda gg: ((gg + 1) * W + S - 1) // S - 1  # noqa: E731
+    local = {}
+    for c, d in enumerate(desc):
+        if d["nsteps"] == 0:
+            continue
+        w0, w1 = wave_of(d["g"]), wave_of(d["g"] + d["nsteps"] - 1)
+        assert (cw[c, 0], cw[c, 1]) == (w0, w1), c
+        npieces = sum(1 for w in range(w0, w1 + 1) if start(w) < start(w + 1))
+        assert cw[c, 2] == npieces, c
+        local[c] = npieces > 1 and w0 // 16 == w1 // 16
+    n_fold = n_pub = 0
+    for w in range(W):
+        g0, g1 = start(w), start(w + 1)
+        want = 0
+        if g0 < g1:
+            first = desc[wc[w]]
+            if first["g"] < g0 and first["g"] + first["nsteps"] <= g1 and local[wc[w]]:
+                want |= 1 | ((w - wave_of(first["g"])) << 8)
+            cl = max(c for c, d in enumerate(desc) if d["nsteps"] and d["g"] < g1)
+            if desc[cl]["g"] + desc[cl]["nsteps"] > g1 and local[cl]:
+                want |= 2
+        assert wf[w] == want, w
+        n_fold += want & 1
+        n_pub += (want >> 1) & 1
+    assert n_fold == sum(local.values())
+    if kind == "cfg2":
+        # 100-step chunks, 25 steps per wave: every chunk is split over 4
+        # waves of one workgroup.
+        assert n_fold == 1024 and n_pub == 3 * 1024

@@ -16,6 +16,7 @@ def main():
     import chunkio_amd as cio
     from chunkio_amd import workloads as wl
     cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
+    tag = sys.argv[2] if len(sys.argv) > 2 else cfg
     lens = wl.cfg2_lens() if cfg == "cfg2" else np.full(1024, 4 << 20, np.uint64)
     offs = wl.packed_offsets(lens, align=16)
     dev = torch.device("cuda:0")
@@ -72,6 +73,11 @@ def main():
         print("   WG max done", q(wg.max(1)))
         print("   WG min done", q(wg.min(1)))
         print("   WG spread  ", q(wg.max(1) - wg.min(1)))
+        ex = us[:, 3].reshape(-1, 16)
+        print("   WG exit - WG max done", q(ex.max(1) - wg.max(1)))
+        last = int(np.argmax(us[:, 3]))
+        print(f"   last exit: wave {last} (WG {last // 16}): stream done {us[last, 2]:.2f}, WG max done "
+              f"{wg.max(1)[last // 16]:.2f}, exit {us[last, 3]:.2f}")
         # rank of wave within its WG (by finish) vs wave index in WG
         order = np.argsort(wg, axis=1)
         print("   mean finish by wave slot", " ".join(f"{x:5.1f}" for x in wg.mean(0)))
@@ -85,8 +91,8 @@ def main():
         print("   corr(entry, done) per WG  %.3f" % np.corrcoef(ent.min(1), wg.max(1))[0, 1])
         out_dir = os.path.join(ROOT, "gpurun_out")
         if os.path.isdir(out_dir):
-            np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}.npy"), us)
-            np.save(os.path.join(out_dir, f"stamps_{cfg}_{it}_hw.npy"), raw[:, 4:6])
+            np.save(os.path.join(out_dir, f"stamps_{tag}_{it}.npy"), us)
+            np.save(os.path.join(out_dir, f"stamps_{tag}_{it}_hw.npy"), raw[:, 4:6])
 
 
 if __name__ == "__main__":
