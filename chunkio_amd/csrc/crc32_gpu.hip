@@ -1199,11 +1199,30 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
         }
         acc = u32x4{x0, x1, x2, x3};
     };
+    // diagnostic (CIO_GPU_RS_LANE): lane l reads 32 or 64 contiguous bytes of
+    // each half / whole step (2 or 4 dwordx4 loads at a 32 / 64-byte lane
+    // stride) instead of 16 bytes of each 1 KiB row.
+    const uint32_t lsh = work >> 16;
+    work &= 0xffffu;
     auto step = [&](uint64_t g) {
-        const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * kGran);
+        if (lsh == 0) {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * kGran);
 #pragma unroll
-        for (int q = 0; q < kSub; ++q) {
-            acc ^= __builtin_nontemporal_load(p + q * kWave);
+            for (int q = 0; q < kSub; ++q) {
+                acc ^= __builtin_nontemporal_load(p + q * kWave);
+            }
+        } else if (lsh == 1) {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * 32u);
+            acc ^= __builtin_nontemporal_load(p);
+            acc ^= __builtin_nontemporal_load(p + 1);
+            acc ^= __builtin_nontemporal_load(p + 128);
+            acc ^= __builtin_nontemporal_load(p + 129);
+        } else {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * 64u);
+#pragma unroll
+            for (int q = 0; q < kSub; ++q) {
+                acc ^= __builtin_nontemporal_load(p + q);
+            }
         }
         burn();
     };
@@ -1918,7 +1937,12 @@ int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
     }
     uint32_t work = 0;
     if (const char *r = getenv("CIO_GPU_RS_WORK")) {
-        work = (uint32_t) std::max(0, atoi(r));
+        work = (uint32_t) std::max(0, std::min(65535, atoi(r)));
+    }
+    if (const char *r = getenv("CIO_GPU_RS_LANE")) {
+        // diagnostic: bytes per lane and step-row, 16 (coalesced rows), 32 or 64
+        const int lb = atoi(r);
+        work |= (lb == 64 ? 2u : lb == 32 ? 1u : 0u) << 16;
     }
     hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream),
