@@ -162,11 +162,22 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
     return ((uint64_t) hi << 32) | lo;
 }
 
-// The plan guarantees S < 2^40 and W <= 2^12 (plan_create), so both
-// numerators stay below 2^52.
+// floor(w * X / W), the even split of X units over W waves.  The plan
+// guarantees S < 2^40 and W <= 2^12 (plan_create), so w * X < 2^52.  A full
+// MI355X has W = 256 x 16 = 2^12 waves: then it is a uniform multiply and
+// shift on the scalar unit, and the kernels' first HBM requests wait on no
+// floating-point division.
+__device__ __forceinline__ uint64_t split_point(uint64_t w, uint64_t X, uint64_t W)
+{
+    if ((W & (W - 1)) == 0) {
+        return (w * X) >> __builtin_ctzll(W);
+    }
+    return div_u52(w * X, W);
+}
+
 __device__ __forceinline__ uint64_t wave_start(uint64_t w, uint64_t S, uint64_t W)
 {
-    return div_u52(w * S, W);
+    return split_point(w, S, W);
 }
 
 // Slice tables in LDS, replicated 32x so lane l always reads bank (l & 31):
@@ -444,6 +455,15 @@ __device__ __forceinline__ uint32_t load_vec_u32(const uint32_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// *p as a per-lane (VGPR) value: the index is an opaque zero, so the compiler
+// cannot treat the load as uniform and read its result into an SGPR at once.
+__device__ __forceinline__ uint32_t load_lane_u32(const uint32_t *p)
+{
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return p[z];
+}
+
 // x ^ (m & c) as one v_bitop3_b32 (truth table 0x78 over x, m, c).
 __device__ __forceinline__ uint32_t xor_and(uint32_t x, uint32_t m, uint32_t c)
 {
@@ -539,14 +559,14 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
-                    uint32_t W, uint32_t unsteps, uint32_t uh,
+                    uint32_t W, uint32_t unsteps, uint32_t uh, uint32_t n,
                     const ChunkDesc *__restrict__ desc,
                     const WaveStart *__restrict__ wstart, const uint32_t *__restrict__ tiny,
                     const uint32_t *__restrict__ seeds, uint32_t *out, const uint32_t *__restrict__ cid,
                     unsigned long long *__restrict__ partials, uint32_t *__restrict__ counters,
                     const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
                     const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ pfac,
-                    uint32_t n, uint32_t ntiny, unsigned long long *stamps = nullptr)
+                    uint32_t ntiny, unsigned long long *stamps)
 {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
@@ -577,7 +597,8 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             // Uniform batch (equal lengths, constant 16-byte-multiple stride):
             // the first chunk and its descriptor follow from the kernel
             // arguments, so the first loads wait on no memory access.
-            c = __builtin_amdgcn_readfirstlane((uint32_t) div_u52(g0, unsteps));
+            // S = n * unsteps, so floor(g0 / unsteps) = floor(wave * n / W).
+            c = __builtin_amdgcn_readfirstlane((uint32_t) split_point(wave, n, W));
             d.a = ua0 + (uint64_t) c * ustride;
             d.vlen = uvlen;
             d.g = (uint64_t) c * unsteps;
@@ -668,9 +689,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // The plan's per-wave words follow the piece slots: the LDS-fold flags
     // (kWfFold, kWfPublish) and the fold factor of the wave's last piece
     // (x^(8 * chunk bytes after it); 1 when that piece ends its chunk).
+    // Loaded as per-lane values: a uniform load's result would be moved to an
+    // SGPR right here, and that wait (vmcnt, in order) would hold the table
+    // build until the first step's data had landed.
     const uint32_t *wwords = pfac + (W + n + 1);
-    const uint32_t wfl = CIO_LDS_FOLD ? load_vec_u32(wwords + wave) : 0u;
-    const uint32_t wlast = load_vec_u32(wwords + W + wave);
+    const uint32_t wfl = CIO_LDS_FOLD ? load_lane_u32(wwords + wave) : 0u;
+    const uint32_t wlast = load_lane_u32(wwords + W + wave);
     uint32_t fold_own = 0, pub = 0;
     // Keep the scheduler from sinking these loads below the table build (and
     // the table arithmetic from rising above them: the first step's HBM
@@ -818,7 +842,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                 rotate_prio(slot_group, it);
             }
             if (it == it_f) {
-                xlast = multmodp(xl, wlast);
+                // (The asm keeps the compiler from hoisting the multiply to
+                // the loop's preheader, where it waited for these loads and
+                // delayed every wave's first step.)
+                uint32_t wl = wlast;
+                asm volatile("" : "+v"(wl));
+                xlast = multmodp(wl, xl);
             }
             const bool pe = crc_step(cur);
             if (STAMPS && it == 0) {
@@ -999,8 +1028,8 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     const uint32_t lb_lo = (lane & 31u) << 2;
     const uint32_t lb_hi = lb_lo | 0x10000u;
     const uint32_t lrep = (lane & 7u) << 2;
-    const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t) div_u52((uint64_t) wave * n, W));
-    const uint32_t c1 = __builtin_amdgcn_readfirstlane((uint32_t) div_u52((uint64_t) (wave + 1) * n, W));
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t) split_point(wave, n, W));
+    const uint32_t c1 = __builtin_amdgcn_readfirstlane((uint32_t) split_point((uint64_t) wave + 1, n, W));
     const uint32_t lbyte = lane * kGran;
     // Valid dummy address for the optional seeds (the value is discarded).
     const uint32_t *const seeds_p = seeds ? seeds : g_x8;
@@ -1446,7 +1475,7 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v7 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains "
+    return "chunkio_amd crc32 v8 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains division-free-start "
            "slice4-lds32x perm horner-fold direct-whole preshifted-partials wg-lds-fold) small(dpp-reduce bitop3-fold) "
            "host(nt-staging graduated-groups pread-bounce multi-device)";
 }
@@ -1825,9 +1854,9 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
     auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
-                       p->W, p->unsteps, p->uh, p->desc, p->wstart, p->tiny,
+                       p->W, p->unsteps, p->uh, p->n, p->desc, p->wstart, p->tiny,
                        dev_seeds, dev_out, cid, p->partials, p->counters, st->slice, st->shift,
-                       st->x8, p->pfac, p->n, p->ntiny, p->stamps);
+                       st->x8, p->pfac, p->ntiny, p->stamps);
     HIP_TRY(hipGetLastError(), "crc32_stream_kernel launch");
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");
