@@ -1015,12 +1015,14 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
 template <bool UNI, bool SEEDS>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t uvlen, uint32_t uh,
-                   uint32_t W, uint32_t n, uint32_t ntiny, const ChunkDesc *__restrict__ desc,
+                   uint32_t W, uint32_t n, uint32_t ntiny, const uint32_t *__restrict__ g_x8,
+                   const ChunkDesc *__restrict__ desc,
                    const uint32_t *__restrict__ tiny, const uint32_t *__restrict__ seeds, uint32_t *out,
-                   const uint32_t *__restrict__ g_x8, const uint32_t *__restrict__ g_xinv8)
+                   const uint32_t *__restrict__ g_xinv8)
 {
-    // (n and ntiny come before the pointers: the first eight arguments are
-    // preloaded into SGPRs, so the first requests wait on no argument load.)
+    // (n, ntiny and g_x8 come first: the first nine arguments are preloaded
+    // into SGPRs, so neither the first data requests nor the lane factor's
+    // load wait on an argument load.)
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
@@ -1844,7 +1846,7 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
                              : (dev_seeds ? crc32_small_kernel<false, true> : crc32_small_kernel<false, false>);
         hipLaunchKernelGGL(sk, dim3(p->grid), dim3(kThreads), 0, s,
                            reinterpret_cast<const uint8_t *>(dev_base), p->ustride, p->ua0, p->uvlen, p->uh,
-                           p->W, p->n, p->ntiny, p->desc, p->tiny, dev_seeds, dev_out, st->x8, st->xinv8);
+                           p->W, p->n, p->ntiny, st->x8, p->desc, p->tiny, dev_seeds, dev_out, st->xinv8);
         HIP_TRY(hipGetLastError(), "crc32_small_kernel launch");
         if (ev1) {
             HIP_TRY(hipEventRecord(ev1, s), "hipEventRecord");
