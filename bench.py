@@ -473,7 +473,7 @@ def run_e2e(args, rank, world, device, dist):
         out = cio.crc32_batch_host_packed(host, offs, lens)
     barrier(dist)
     t0 = time.perf_counter()
-    steps = max(1, min(args.steps, 10))
+    steps = max(1, min(args.steps, 30))
     for _ in range(steps):
         out = cio.crc32_batch_host_packed(host, offs, lens)
     barrier(dist)
@@ -804,7 +804,7 @@ def other_configs(args, rank, world, device, dist):
     import torch
     out = {}
     t0 = time.perf_counter()
-    for cfg, steps, warm in (("cfg3", 5, 2), ("sha1", 10, 2), ("e2e", 10, 10)):
+    for cfg, steps, warm in (("cfg3", 5, 2), ("sha1", 10, 2), ("e2e", 30, 10)):
         torch.cuda.empty_cache()
         a = copy.copy(args)
         a.config, a.steps, a.warmup, a.no_cpu = cfg, steps, warm, True
