@@ -1517,6 +1517,14 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
         p->prio = (v == 0) ? 0 : 1;
     }
     p->grid = (uint32_t) st->cus;
+    // Test knob: fewer workgroups than CUs (e.g. a wave count that is not a
+    // power of two, which takes the kernels' f64 split instead of the shift).
+    if (const char *r = getenv("CIO_GPU_GRID")) {
+        const int v = atoi(r);
+        if (v >= 1 && v < (int) p->grid) {
+            p->grid = (uint32_t) v;
+        }
+    }
     p->W = p->grid * (kThreads / kWave);
 }
 

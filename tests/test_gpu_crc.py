@@ -196,6 +196,27 @@ def test_workgroup_local_and_cross_workgroup_pieces(cuda, kind):
                                   po.crc_batch(buf, offs, lens, seeds=seeds))
 
 
+@pytest.mark.parametrize("grid", [3, 4, 17])
+def test_reduced_grid_split_paths(cuda, monkeypatch, grid):
+    """Plans on fewer workgroups (CIO_GPU_GRID): 48 and 272 waves take the
+    kernels' f64 even split, 64 the shift; uniform (stream and small kernel)
+    and mixed batches, workgroup-local and cross-workgroup pieces, seeds."""
+    monkeypatch.setenv("CIO_GPU_GRID", str(grid))
+    rng = np.random.default_rng(grid)
+    cases = [np.full(300, 409600, np.uint64),                      # uniform, stream kernel
+             np.full(5000, 4096, np.uint64),                       # uniform, small kernel
+             rng.integers(0, 300_000, 700).astype(np.uint64),      # mixed, tiny chunks too
+             rng.integers(1, 4096, 3000).astype(np.uint64)]        # mixed, small kernel
+    for k, lens in enumerate(cases):
+        buf, offs = wl.host_batch(0x6A1D + k, lens, align=16)
+        if k >= 2:
+            offs = offs + rng.integers(0, 16, len(offs)).astype(np.uint64)
+            buf = np.concatenate([buf, np.zeros(32, np.uint8)])
+        seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+        np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds),
+                                      po.crc_batch(buf, offs, lens, seeds=seeds), err_msg=str(k))
+
+
 def test_one_huge_chunk_spans_all_waves(cuda):
     n = 48 * 1024 * 1024 + 12345
     data = wl.gen_chunk(0xBEEF, 0, n)

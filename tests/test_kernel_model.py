@@ -147,7 +147,7 @@ def _layout(offs, lens, W):
     return cw.reshape(-1, 3), wf
 
 
-@pytest.mark.parametrize("W,kind", [(4096, "cfg2"), (4096, "mixed"), (4096, "fewer_steps"), (256, "mixed")])
+@pytest.mark.parametrize("W,kind", [(4096, "cfg2"), (4096, "mixed"), (4096, "fewer_steps"), (256, "mixed"), (48, "mixed")])
 def test_plan_workgroup_local_fold_flags(W, kind):
     """The C plan's per-chunk wave range (w0, w1) and per-wave LDS-fold flags
     (crc32_gpu.hip plan_build) against a restatement of their definition:
