@@ -12,6 +12,7 @@ Run from the repo root:  python tests/golden/make_golden.py
 """
 import hashlib
 import json
+import multiprocessing
 import os
 import sys
 import zlib
@@ -35,6 +36,10 @@ def ref_raw(seed, data):
         z = zlib.crc32(bytes(data)) ^ 0xFFFFFFFF
         assert r == z, (hex(r), hex(z))
     return r
+
+
+def _cfg4_raw(i):
+    return ref_raw(INIT, wl.gen_chunk(wl.CFG4_SEED, i, wl.CFG4_LEN).tobytes())
 
 
 def main():
@@ -92,11 +97,15 @@ def main():
                    "sample_idx": idx3,
                    "sample_raw": [ref_raw(INIT, wl.gen_chunk(wl.CFG3_SEED, i, int(l3[i])).tobytes())
                                   for i in idx3]}
-    # Config 4: raw CRCs of 8 chunks (one per GPU shard at G=8).
+    # Config 4: raw CRCs of 8 chunks (one per GPU shard at G=8), and a digest of
+    # all 8192 (34.4 GB through the reference crc32.c and zlib, 6 processes),
+    # so the sharded full-size job can be checked whole.
+    with multiprocessing.Pool(6) as pool:
+        c4 = pool.map(_cfg4_raw, range(wl.CFG4_N), chunksize=64)
     out["cfg4"] = {"seed": wl.CFG4_SEED, "n": wl.CFG4_N, "len": wl.CFG4_LEN,
                    "sample_idx": list(range(8)),
-                   "sample_raw": [ref_raw(INIT, wl.gen_chunk(wl.CFG4_SEED, i, wl.CFG4_LEN).tobytes())
-                                  for i in range(8)]}
+                   "sample_raw": c4[:8],
+                   "sha256_of_raw_le": hashlib.sha256(np.asarray(c4, np.uint32).tobytes()).hexdigest()}
     # SHA-1 (config 5): hashlib (OpenSSL) -- the reference's <sha1/sha1.h> is not vendored.
     out["sha1"] = {"oracle": "hashlib.sha1 (OpenSSL); FIPS 180-4 KATs",
                    "kats": [{"hex": b"abc".hex(), "digest": hashlib.sha1(b"abc").hexdigest()},

@@ -308,6 +308,33 @@ def test_cfg4_shard_golden(cuda, golden):
     split_combine_check(cuda, dev, offs, lens, got)
 
 
+def test_cfg4_full_job_sharded_g1_2_4_8(cuda, golden):
+    """BASELINE config 4 at full size (8192 x 4 MiB = 34.4 GB) as the G = 1, 2, 4
+    and 8 GPU jobs see it: shard r holds chunks r, r+G, ... (shard.shard_ids), is
+    filled by generator chunk id into its own packed buffer, and is CRC'd as one
+    batch; shard.assemble scatters the results back to chunk order, and the
+    digest of all 8192 CRCs must equal the one made from the reference crc32.c
+    (tests/golden/make_golden.py).  One GPU runs the shards one after another."""
+    import torch
+    from chunkio_amd import shard
+    g = golden["cfg4"]
+    n, ln = g["n"], g["len"]
+    dev = torch.empty(n * ln, dtype=torch.uint8, device=cuda)
+    for world in (1, 2, 4, 8):
+        parts = []
+        for r in range(world):
+            ids = shard.shard_ids(n, r, world)
+            lens = np.full(len(ids), ln, np.uint64)
+            offs = np.arange(len(ids), dtype=np.uint64) * np.uint64(ln)
+            cio.fill_synthetic(dev, offs, lens, g["seed"], ids=ids)
+            parts.append(cio.crc32_batch_dev(dev, offs, lens))
+        full = shard.assemble(n, world, parts)
+        assert list(map(int, full[:8])) == g["sample_raw"], world
+        assert hashlib.sha256(full.astype("<u4").tobytes()).hexdigest() == g["sha256_of_raw_le"], world
+    del dev
+    torch.cuda.empty_cache()
+
+
 def test_host_batch_end_to_end(cuda, data400):
     rng = np.random.default_rng(10)
     bufs = [np.frombuffer(b"\0\0" + data400, np.uint8)]
