@@ -252,3 +252,13 @@ def sha1_batch_dev(base, offs, lens, stream=None):
                                              _stream_ptr(stream)),
                "cio_sha1_batch_dev")
     return out[: n * 20].cpu().numpy().reshape(n, 20)
+
+
+def sha1_batch_dev_async(base, dev_offs, dev_lens, dev_digests, stream=None):
+    """Launch SHA-1 over a batch whose offsets/lengths are device tensors (int64,
+    n each) into dev_digests (uint8, >= 20 n); no allocation, no sync."""
+    n = int(dev_offs.numel())
+    assert dev_lens.numel() == n and dev_digests.numel() >= 20 * n
+    _lib.check(_lib.lib().cio_sha1_batch_dev_async(_ptr(base), _ptr(dev_offs), _ptr(dev_lens), _ptr(dev_digests),
+                                                   n, _stream_ptr(stream)),
+               "cio_sha1_batch_dev_async")

@@ -110,6 +110,33 @@ __device__ __forceinline__ void message_block(const uint8_t *p, uint64_t len, ui
     }
 }
 
+// The 80 rounds of one block from its K_t + W_t rows, folded into the chaining
+// value: 5 VALU per round (two rotates, v_bitop3 round function, add, add3).
+__device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20])
+{
+#ifdef CIO_SHA1_DIAG_NOROUNDS
+    st.h0 ^= rows[0].x ^ rows[19].w;   // diagnostic: hand-over only, wrong digests
+    return;
+#endif
+    uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        const uint32_t kwv[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * r + u;
+            const uint32_t f = t < 20 ? ch3(b, c, d) : (t < 40 || t >= 60) ? xor3(b, c, d) : maj3(b, c, d);
+            const uint32_t tmp = rotl(a, 5) + f + e + kwv[u];
+            e = d;
+            d = c;
+            c = rotl(b, 30);
+            b = a;
+            a = tmp;
+        }
+    }
+    st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+}
+
 // One workgroup = two waves on two SIMDs for the same 64 chunks (one per
 // lane).  Wave 1 (schedule) loads each 64-byte block, expands the message
 // schedule and writes K_t + W_t for the 80 rounds to LDS; wave 0 (rounds)
@@ -121,12 +148,52 @@ __device__ __forceinline__ void message_block(const uint8_t *p, uint64_t len, ui
 // rounds run, one barrier per block.
 constexpr int kShaRowsPerBlock = 20;   // 80 rounds as 20 rows of 4 (ds_read/write_b128)
 constexpr int kShaAhead = 4;           // blocks of message data in flight on the schedule wave
+#ifdef CIO_SHA1_GROUP
+constexpr int kShaPer = CIO_SHA1_GROUP;   // blocks handed over per barrier
+#else
+constexpr int kShaPer = 1;
+#endif
+static_assert(kShaAhead % kShaPer == 0, "a hand-over group must not straddle the prefetch ring");
+#if defined(CIO_SHA1_FLAGS)
+// Hand-over by LDS flags instead of barriers: slot k % kShaSlots holds block k;
+// ready[slot] = k + 1 once its rows are written, consumed = number of blocks
+// the round wave has read into registers.  No wave ever waits at a barrier.
+constexpr int kShaSlots = 4;
+constexpr uint32_t kShaSpinBudget = 1u << 20;  // polls per wave per launch (~30x a launch's need): a wedge ends in ms
+#elif defined(CIO_SHA1_PREFETCH)
+// Three slots: block j + 1 is in LDS before barrier j, so the round wave reads
+// it into registers while it runs block j and never waits on LDS latency.
+static_assert(kShaPer == 1, "row prefetch hands over one block per barrier");
+constexpr int kShaSlots = 3;
+#else
+constexpr int kShaSlots = 2 * kShaPer; // LDS slots: one hand-over being read, one being written
+#endif
+
+__device__ __forceinline__ void sha1_load_rows(uint4 (&rows)[20], const uint4 *row)
+{
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        rows[r] = row[r * 64];
+    }
+}
 
 __global__ void __launch_bounds__(128)
 sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests, uint32_t n)
 {
-    __shared__ uint4 kw[2][kShaRowsPerBlock][64];   // [slot][t / 4][lane] = K + W for t..t+3
+    __shared__ uint4 kw[kShaSlots][kShaRowsPerBlock][64];   // [slot][t / 4][lane] = K + W for t..t+3
+#ifdef CIO_SHA1_FLAGS
+    __shared__ uint32_t ready[kShaSlots];
+    __shared__ uint32_t consumed;
+    if (threadIdx.x < kShaSlots) {
+        ready[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) {
+        consumed = 0;
+    }
+    uint32_t budget = kShaSpinBudget;
+    __syncthreads();
+#endif
     const uint32_t lane = threadIdx.x & 63u;
     const bool sched = threadIdx.x >= 64;
     const uint32_t i = blockIdx.x * 64 + lane;
@@ -156,7 +223,12 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint64_t b = (uint64_t) u < full ? (uint64_t) u : (full ? full - 1 : 0);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
+#ifdef CIO_SHA1_DIAG_NOLOAD
+                nx[u][v] = make_uint4(0, 0, 0, 0);
+                (void) b;
+#else
                 nx[u][v] = (aligned && full > 0) ? q[b * 4 + v] : make_uint4(0, 0, 0, 0);
+#endif
             }
         }
         auto produce = [&](uint64_t j, uint4 (&r)[4]) {
@@ -164,6 +236,14 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 return;
             }
             uint32_t w[16];
+#ifdef CIO_SHA1_DIAG_NOLOAD
+            if (true) {   // diagnostic: schedule from stand-in words, no HBM reads, wrong digests
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    w[t] = (uint32_t) j * 0x9E3779B9u + lane * 16u + (uint32_t) t;
+                }
+            } else
+#endif
             if (aligned && j < full) {
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
@@ -179,7 +259,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             } else {
                 message_block(p, len, full, j, w);
             }
-            uint4 *row = &kw[j & 1][0][lane];
+            uint4 *row = &kw[j % kShaSlots][0][lane];
 #pragma unroll
             for (int r = 0; r < kShaRowsPerBlock; ++r) {
                 uint32_t v[4];
@@ -198,53 +278,185 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 row[r * 64] = make_uint4(v[0], v[1], v[2], v[3]);
             }
         };
-        // Block j's schedule is written before barrier j (wmax + 1 barriers,
-        // as on the round wave); unrolled so each ring slot is a fixed register set.
-        for (uint64_t jb = 0; jb <= wmax; jb += kShaAhead) {
+#if defined(CIO_SHA1_FLAGS)
+        for (uint64_t jb = 0; jb < wmax; jb += kShaAhead) {
 #pragma unroll
             for (int u = 0; u < kShaAhead; ++u) {
-                if (jb + u <= wmax) {
-                    produce(jb + u, nx[u]);
-                    __syncthreads();
+                const uint64_t k = jb + u;
+                if (k < wmax) {
+                    // Slot k % kShaSlots is free once block k - kShaSlots is in
+                    // the round wave's registers.
+                    while (k >= (uint64_t) kShaSlots && budget > 0 &&
+                           __builtin_amdgcn_readfirstlane(__hip_atomic_load(&consumed, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) <
+                               (uint32_t) (k - kShaSlots + 1)) {
+                        --budget;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    produce(k, nx[u]);
+                    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the rows are in LDS before the flag
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    __hip_atomic_store(&ready[k % kShaSlots], (uint32_t) (k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
+#elif defined(CIO_SHA1_PREFETCH)
+        // Blocks 0..j+1 are written before barrier j (j = 0..wmax: wmax + 1
+        // barriers, as on the round wave); unrolled so each ring slot is a
+        // fixed register set.
+        for (uint64_t jb = 0; jb <= wmax + 1; jb += kShaAhead) {
+#pragma unroll
+            for (int u = 0; u < kShaAhead; ++u) {
+                if (jb + u <= wmax + 1) {
+                    produce(jb + u, nx[u]);
+                    if (jb + u >= 1) {
+                        __syncthreads();
+                    }
+                }
+            }
+        }
+#else
+        // Blocks [g kShaPer, (g + 1) kShaPer) are written before barrier g, one
+        // barrier per group as on the round wave; unrolled so each ring slot is
+        // a fixed register set.
+        const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
+        for (uint64_t jb = 0; jb < ngroups * kShaPer; jb += kShaAhead) {
+#pragma unroll
+            for (int u = 0; u < kShaAhead; ++u) {
+                if (jb + u < ngroups * kShaPer) {
+                    produce(jb + u, nx[u]);
+                    if (u % kShaPer == kShaPer - 1) {
+                        __syncthreads();
+                    }
+                }
+            }
+        }
+#endif
         return;
     }
 
     Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
-    __syncthreads();
-    for (uint64_t j = 0; j < wmax; ++j) {
-        if (j < nblk) {
-            const uint4 *row = &kw[j & 1][0][lane];
-            // All 20 rows are requested up front (80 VGPRs; this wave is alone
-            // on its SIMD), so LDS latency is paid once per block, not per row.
-            uint4 rows[kShaRowsPerBlock];
-#pragma unroll
-            for (int r = 0; r < kShaRowsPerBlock; ++r) {
-                rows[r] = row[r * 64];
-            }
-            uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
-#pragma unroll
-            for (int r = 0; r < kShaRowsPerBlock; ++r) {
-                const uint4 q = rows[r];
-                const uint32_t kwv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int t = 4 * r + u;
-                    const uint32_t f = t < 20 ? ch3(b, c, d) : (t < 40 || t >= 60) ? xor3(b, c, d) : maj3(b, c, d);
-                    const uint32_t tmp = rotl(a, 5) + f + e + kwv[u];
-                    e = d;
-                    d = c;
-                    c = rotl(b, 30);
-                    b = a;
-                    a = tmp;
-                }
-            }
-            st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+#if defined(CIO_SHA1_FLAGS)
+    // Block j + 1's flag and rows are read before block j's rounds run, so by
+    // the time they are checked they have landed; LDS serves one wave's
+    // operations in order, so rows read after a flag that says "ready" are the
+    // rows written before it.  A flag read too early is re-read (spin) with
+    // the rows after it.
+    uint4 ra[kShaRowsPerBlock], rb[kShaRowsPerBlock];
+    const uint4 *slot0 = &kw[0][0][lane];
+    constexpr uint32_t kSlotWords = kShaRowsPerBlock * 64;
+    auto fetch = [&](uint64_t k, uint4 (&rows)[kShaRowsPerBlock]) -> uint32_t {
+        const uint32_t f = __hip_atomic_load(&ready[k % kShaSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        sha1_load_rows(rows, slot0 + (uint32_t) (k % kShaSlots) * kSlotWords);
+        return f;
+    };
+    auto settle = [&](uint64_t k, uint32_t f, uint4 (&rows)[kShaRowsPerBlock]) {
+        while (__builtin_amdgcn_readfirstlane(f) != (uint32_t) (k + 1) && budget > 0) {
+            --budget;
+            __builtin_amdgcn_s_sleep(1);
+            f = fetch(k, rows);
         }
-        __syncthreads();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __hip_atomic_store(&consumed, (uint32_t) (k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // The rows were requested a whole block of rounds ago and have landed;
+        // saying so keeps the compiler from waiting on the next prefetch
+        // inside the next block's rounds.
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+    };
+    {
+        const uint32_t f0 = fetch(0, ra);
+        settle(0, f0, ra);
     }
+    for (uint64_t j = 0; j < wmax; j += 2) {
+        const bool more = j + 1 < wmax;
+        uint32_t fb = 0;
+        if (more) {
+            fb = fetch(j + 1, rb);
+        }
+        if (j < nblk) {
+            sha1_block_rounds(st, ra);
+        }
+        if (!more) {
+            break;
+        }
+        settle(j + 1, fb, rb);
+        const bool more2 = j + 2 < wmax;
+        uint32_t fa = 0;
+        if (more2) {
+            fa = fetch(j + 2, ra);
+        }
+        if (j + 1 < nblk) {
+            sha1_block_rounds(st, rb);
+        }
+        if (more2) {
+            settle(j + 2, fa, ra);
+        }
+    }
+#elif defined(CIO_SHA1_PREFETCH)
+    // Ping-pong register sets (no 80-register copies): block j's rows were
+    // read before barrier j; block j + 1's go out before block j's rounds.
+    uint4 ra[kShaRowsPerBlock], rb[kShaRowsPerBlock];
+    const uint4 *slot0 = &kw[0][0][lane];
+    constexpr uint32_t kSlotWords = kShaRowsPerBlock * 64;   // uint4s per slot
+    uint32_t s1 = kSlotWords, s2 = 2 * kSlotWords;          // slots of blocks j + 1, j + 2
+    __syncthreads();                                   // barrier 0: blocks 0, 1
+    sha1_load_rows(ra, slot0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0): no load of ra left in flight at the loop head
+    for (uint64_t j = 0; j < wmax; j += 2) {
+        sha1_load_rows(rb, slot0 + s1);
+        if (j < nblk) {
+            sha1_block_rounds(st, ra);
+        }
+        __syncthreads();                               // barrier j + 1
+        if (j + 1 < wmax) {
+            sha1_load_rows(ra, slot0 + s2);
+            if (j + 1 < nblk) {
+                sha1_block_rounds(st, rb);
+            }
+            __syncthreads();                           // barrier j + 2
+        }
+        // Slots advance by two blocks: (s1, s2) <- (s1 + 2, s2 + 2) mod 3 slots.
+        const uint32_t s0 = 3 * kSlotWords - s1 - s2;
+        s1 = s0;
+        s2 = s1 == 2 * kSlotWords ? 0u : s1 + kSlotWords;
+    }
+#else
+    const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
+    for (uint64_t g = 0; g < ngroups; ++g) {
+        __syncthreads();
+        // All 20 rows of every block of the group are requested up front
+        // (80 VGPRs per block; this wave is alone on its SIMD), so the LDS
+        // latency after the barrier is paid once per group.
+        uint4 rows[kShaPer][kShaRowsPerBlock];
+#pragma unroll
+        for (int u = 0; u < kShaPer; ++u) {
+            const uint4 *row = &kw[(g * kShaPer + u) % kShaSlots][0][lane];
+#pragma unroll
+            for (int r = 0; r < kShaRowsPerBlock; ++r) {
+                rows[u][r] = row[r * 64];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kShaPer; ++u) {
+#ifdef CIO_SHA1_SELECT
+            // Every lane runs the rounds (a wave issues them anyway) and lanes
+            // past their last block keep their state: no branch for the
+            // compiler to sink the row reads into.
+            Sha1State nx = st;
+            sha1_block_rounds(nx, rows[u]);
+            const bool take = g * kShaPer + u < nblk;
+            st.h0 = take ? nx.h0 : st.h0; st.h1 = take ? nx.h1 : st.h1; st.h2 = take ? nx.h2 : st.h2;
+            st.h3 = take ? nx.h3 : st.h3; st.h4 = take ? nx.h4 : st.h4;
+#else
+            if (g * kShaPer + u < nblk) {
+                sha1_block_rounds(st, rows[u]);
+            }
+#endif
+        }
+    }
+#endif
     if (!live) {
         return;
     }
@@ -260,6 +472,34 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
 }
 
 }  // namespace
+
+namespace {
+
+int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens, uint8_t *dev_digests,
+                size_t n, hipStream_t s)
+{
+    if (n > 0xFFFFFFFFull - 63) {
+        return cioa_fail_msg("cio_sha1_batch_dev", "too many chunks for one launch");
+    }
+    hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(128), 0, s,
+                       reinterpret_cast<const uint8_t *>(dev_base), dev_offs, dev_lens, dev_digests, (uint32_t) n);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev: launch", hipGetErrorString(e));
+}
+
+}  // namespace
+
+extern "C" int cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens,
+                                        uint8_t *dev_digests, size_t n, void *stream)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (cio_gpu_init() != CIO_OK) {
+        return CIO_ERROR;
+    }
+    return sha1_launch(dev_base, dev_offs, dev_lens, dev_digests, n, reinterpret_cast<hipStream_t>(stream));
+}
 
 extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, const uint64_t *lens,
                                   uint8_t *dev_digests, size_t n, void *stream)
@@ -280,15 +520,15 @@ extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, co
     if (e == hipSuccess) {
         e = hipMemcpyAsync(d + n, lens, n * sizeof(uint64_t), hipMemcpyHostToDevice, s);
     }
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(128), 0, s,
-                           reinterpret_cast<const uint8_t *>(dev_base), d, d + n, dev_digests,
-                           (uint32_t) n);
-        e = hipGetLastError();
+    if (e != hipSuccess) {
+        (void) hipFree(d);
+        return cioa_fail_msg("cio_sha1_batch_dev: copy", hipGetErrorString(e));
     }
-    if (e == hipSuccess) {
-        e = hipStreamSynchronize(s);
-    }
+    const int rc = sha1_launch(dev_base, d, d + n, dev_digests, n, s);
+    e = hipStreamSynchronize(s);
     (void) hipFree(d);
+    if (rc != CIO_OK) {
+        return rc;
+    }
     return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev", hipGetErrorString(e));
 }

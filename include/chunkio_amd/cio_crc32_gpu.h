@@ -180,6 +180,14 @@ int  cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs,
                         const uint64_t *lens, uint8_t *dev_digests, size_t n,
                         void *stream);
 
+/* The same with DEVICE-resident dev_offs/dev_lens (n entries each): one kernel
+ * launch on `stream`, no allocation, no host synchronisation, so it can be
+ * captured in a HIP graph and repeated over a resident batch like
+ * cio_crc32_plan_exec. */
+int  cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *dev_offs,
+                              const uint64_t *dev_lens, uint8_t *dev_digests,
+                              size_t n, void *stream);
+
 /* ---- diagnostics -------------------------------------------------------- */
 
 /* Read-only stream over floor(bytes / 4096) * 4096 bytes of dev_base with the

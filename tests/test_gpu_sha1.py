@@ -48,3 +48,36 @@ def test_cfg5_sample(cuda, golden, data400):
     assert [bytes(d).hex() for d in got[:8]] == golden["sha1"]["cfg2_first8"]
     got400 = run(cuda, [data400])
     assert bytes(got400[0]).hex() == golden["sha1"]["400kb"]
+
+
+def test_async_device_descriptors(cuda, golden):
+    """cio_sha1_batch_dev_async (device-resident offsets/lengths, no sync) gives
+    the digests of the synchronous entry on the full cfg5 batch, repeated on one
+    stream, and on ragged lengths whose lanes end at different blocks."""
+    import torch
+    lens = wl.cfg2_lens()
+    offs = wl.packed_offsets(lens, align=16)
+    dev = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, wl.CFG2_SEED)
+    want = cio.sha1_batch_dev(dev, offs, lens)
+    assert [bytes(d).hex() for d in want[:8]] == golden["sha1"]["cfg2_first8"]
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(cuda)
+    d_lens = torch.from_numpy(lens.astype(np.int64)).to(cuda)
+    out = torch.zeros(len(lens) * 20, dtype=torch.uint8, device=cuda)
+    for _ in range(3):
+        cio.sha1_batch_dev_async(dev, d_offs, d_lens, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(-1, 20), want)
+
+    rng = np.random.default_rng(22)
+    rl = rng.integers(0, 20000, 200).astype(np.uint64)
+    ro = wl.packed_offsets(rl)
+    rdev = torch.empty(wl.batch_bytes(ro, rl) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(rdev, ro, rl, 0x5A1)
+    rout = torch.zeros(len(rl) * 20, dtype=torch.uint8, device=cuda)
+    cio.sha1_batch_dev_async(rdev, torch.from_numpy(ro.astype(np.int64)).to(cuda),
+                             torch.from_numpy(rl.astype(np.int64)).to(cuda), rout)
+    got = rout.cpu().numpy().reshape(-1, 20)
+    host = rdev.cpu().numpy()
+    for i in range(len(rl)):
+        assert bytes(got[i]) == hashlib.sha1(host[int(ro[i]):int(ro[i] + rl[i])].tobytes()).digest(), i
