@@ -9,8 +9,8 @@
 // SHA-1 cannot be split inside a message (each 64-byte block depends on the
 // previous chaining value), so the unit of parallelism is one chunk per lane:
 // 1024 chunks = 16 round waves.  This config is bound by the dependent round
-// chain, not by HBM; DESIGN.md reports it as such.  The message schedule runs
-// on a second wave (sha1_kernel).
+// chain's issue rate, not by HBM; DESIGN.md reports it as such.  The message
+// schedule runs on two more waves (sha1_kernel).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -114,10 +114,6 @@ __device__ __forceinline__ void message_block(const uint8_t *p, uint64_t len, ui
 // value: 5 VALU per round (two rotates, v_bitop3 round function, add, add3).
 __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20])
 {
-#ifdef CIO_SHA1_DIAG_NOROUNDS
-    st.h0 ^= rows[0].x ^ rows[19].w;   // diagnostic: hand-over only, wrong digests
-    return;
-#endif
     uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
 #pragma unroll
     for (int r = 0; r < 20; ++r) {
@@ -137,65 +133,45 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
     st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
 }
 
-// One workgroup = two waves on two SIMDs for the same 64 chunks (one per
-// lane).  Wave 1 (schedule) loads each 64-byte block, expands the message
-// schedule and writes K_t + W_t for the 80 rounds to LDS; wave 0 (rounds)
-// runs only the dependent round chain, 5 instructions per round (rotate,
-// v_bitop3 round function, add3, add, rotate) instead of 7.5 with the schedule
-// inline.  The round chain of one chunk is the bound (one wave per SIMD, one
-// VALU instruction per 4 cycles), so halving its instruction stream is the
-// speed-up; two LDS slots let block j+1's schedule be built while block j's
-// rounds run, one barrier per block.
-constexpr int kShaRowsPerBlock = 20;   // 80 rounds as 20 rows of 4 (ds_read/write_b128)
-constexpr int kShaAhead = 4;           // blocks of message data in flight on the schedule wave
+// One workgroup = one round wave + kShaSched schedule waves for the same 64
+// chunks (one chunk per lane), each wave alone on its SIMD.
+//  - Schedule wave s loads blocks j = s, s + kShaSched, ... (kShaAhead of its
+//    own blocks in flight), byte-swaps them, expands the message schedule and
+//    writes K_t + W_t for the 80 rounds to LDS.
+//  - The round wave runs only the dependent round chain, 5 VALU per round.
+// A lone wave issues one VALU instruction per ~4 cycles
+// (tools/probe/sha1_round_probe.hip: 20.35 cycles per 5-instruction round, in
+// any dependency order), so a chain's floor is ~1630 cycles per block.  One
+// schedule wave needed more than that per block (~250 instructions plus its
+// LDS writes: a build whose round wave did no rounds took 4.5 ms per cfg5
+// batch), so it, not the chain, set the pace; two schedule waves halve it.
+// Blocks are handed over kShaPer at a time through 2 kShaPer LDS slots, one
+// barrier per group (a barrier per block cost ~3 cycles per round).
 #ifdef CIO_SHA1_GROUP
-constexpr int kShaPer = CIO_SHA1_GROUP;   // blocks handed over per barrier
+constexpr int kShaPer = CIO_SHA1_GROUP;           // blocks handed over per barrier
 #else
-constexpr int kShaPer = 1;
+constexpr int kShaPer = 2;
 #endif
-static_assert(kShaAhead % kShaPer == 0, "a hand-over group must not straddle the prefetch ring");
-#if defined(CIO_SHA1_FLAGS)
-// Hand-over by LDS flags instead of barriers: slot k % kShaSlots holds block k;
-// ready[slot] = k + 1 once its rows are written, consumed = number of blocks
-// the round wave has read into registers.  No wave ever waits at a barrier.
-constexpr int kShaSlots = 4;
-constexpr uint32_t kShaSpinBudget = 1u << 20;  // polls per wave per launch (~30x a launch's need): a wedge ends in ms
-#elif defined(CIO_SHA1_PREFETCH)
-// Three slots: block j + 1 is in LDS before barrier j, so the round wave reads
-// it into registers while it runs block j and never waits on LDS latency.
-static_assert(kShaPer == 1, "row prefetch hands over one block per barrier");
-constexpr int kShaSlots = 3;
+#ifdef CIO_SHA1_SCHED_WAVES
+constexpr int kShaSched = CIO_SHA1_SCHED_WAVES;   // schedule waves
 #else
-constexpr int kShaSlots = 2 * kShaPer; // LDS slots: one hand-over being read, one being written
+constexpr int kShaSched = 2;
 #endif
+constexpr int kShaRowsPerBlock = 20;              // 80 rounds as 20 rows of 4 (ds_read/write_b128)
+constexpr int kShaAhead = 4;                      // own blocks in flight per schedule wave
+constexpr int kShaSlots = 2 * kShaPer;            // one group being read, one being written
+constexpr int kShaThreads = 64 * (1 + kShaSched);
+static_assert(kShaPer % kShaSched == 0, "every schedule wave builds the same number of blocks per group");
+static_assert((kShaAhead * kShaSched) % kShaPer == 0, "a ring turn covers whole groups");
 
-__device__ __forceinline__ void sha1_load_rows(uint4 (&rows)[20], const uint4 *row)
-{
-#pragma unroll
-    for (int r = 0; r < 20; ++r) {
-        rows[r] = row[r * 64];
-    }
-}
-
-__global__ void __launch_bounds__(128)
+__global__ void __launch_bounds__(kShaThreads)
 sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests, uint32_t n)
 {
     __shared__ uint4 kw[kShaSlots][kShaRowsPerBlock][64];   // [slot][t / 4][lane] = K + W for t..t+3
-#ifdef CIO_SHA1_FLAGS
-    __shared__ uint32_t ready[kShaSlots];
-    __shared__ uint32_t consumed;
-    if (threadIdx.x < kShaSlots) {
-        ready[threadIdx.x] = 0;
-    }
-    if (threadIdx.x == 0) {
-        consumed = 0;
-    }
-    uint32_t budget = kShaSpinBudget;
-    __syncthreads();
-#endif
     const uint32_t lane = threadIdx.x & 63u;
     const bool sched = threadIdx.x >= 64;
+    const uint32_t sw = sched ? (threadIdx.x >> 6) - 1 : 0;   // this schedule wave's block residue
     const uint32_t i = blockIdx.x * 64 + lane;
     const bool live = i < n;
     const uint32_t ic = live ? i : n - 1;
@@ -209,26 +185,24 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     for (int o = 32; o >= 1; o >>= 1) {
         wmax = max(wmax, (uint64_t) __shfl_xor((unsigned long long) wmax, o));
     }
+    const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
 
     if (sched) {
         // Aligned content blocks come from a kShaAhead-deep register ring
-        // (block j + kShaAhead is requested when block j is consumed): the 64
-        // lanes read 64 chunks far apart, and one block of prefetch did not
-        // cover the HBM latency.
+        // (this wave's block j + kShaAhead kShaSched is requested when block j
+        // is consumed): the 64 lanes read 64 chunks far apart, and one block
+        // of prefetch did not cover the HBM latency.
         const bool aligned = ((uintptr_t) p & 15u) == 0;
         const uint4 *q = reinterpret_cast<const uint4 *>(p);
+        constexpr uint64_t kStride = (uint64_t) kShaAhead * kShaSched;
         uint4 nx[kShaAhead][4];
 #pragma unroll
         for (int u = 0; u < kShaAhead; ++u) {
-            const uint64_t b = (uint64_t) u < full ? (uint64_t) u : (full ? full - 1 : 0);
+            const uint64_t ub = sw + (uint64_t) u * kShaSched;   // this wave's u-th block
+            const uint64_t b = ub < full ? ub : (full ? full - 1 : 0);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-#ifdef CIO_SHA1_DIAG_NOLOAD
-                nx[u][v] = make_uint4(0, 0, 0, 0);
-                (void) b;
-#else
                 nx[u][v] = (aligned && full > 0) ? q[b * 4 + v] : make_uint4(0, 0, 0, 0);
-#endif
             }
         }
         auto produce = [&](uint64_t j, uint4 (&r)[4]) {
@@ -236,21 +210,13 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 return;
             }
             uint32_t w[16];
-#ifdef CIO_SHA1_DIAG_NOLOAD
-            if (true) {   // diagnostic: schedule from stand-in words, no HBM reads, wrong digests
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    w[t] = (uint32_t) j * 0x9E3779B9u + lane * 16u + (uint32_t) t;
-                }
-            } else
-#endif
             if (aligned && j < full) {
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     w[4 * v + 0] = bswap32(r[v].x); w[4 * v + 1] = bswap32(r[v].y);
                     w[4 * v + 2] = bswap32(r[v].z); w[4 * v + 3] = bswap32(r[v].w);
                 }
-                const uint64_t pf = j + kShaAhead < full ? j + kShaAhead : full - 1;   // clamped
+                const uint64_t pf = j + kStride < full ? j + kStride : full - 1;   // clamped
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     r[v] = q[pf * 4 + v];
@@ -278,157 +244,30 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 row[r * 64] = make_uint4(v[0], v[1], v[2], v[3]);
             }
         };
-#if defined(CIO_SHA1_FLAGS)
-        for (uint64_t jb = 0; jb < wmax; jb += kShaAhead) {
+        // Group g = blocks [g kShaPer, (g + 1) kShaPer) is in LDS before
+        // barrier g: every schedule wave meets the round wave there after its
+        // last block of the group (ngroups barriers per wave).  Unrolled so
+        // each ring slot is a fixed register set.
+        for (uint64_t jb = 0; jb < ngroups * kShaPer; jb += kStride) {
 #pragma unroll
             for (int u = 0; u < kShaAhead; ++u) {
-                const uint64_t k = jb + u;
-                if (k < wmax) {
-                    // Slot k % kShaSlots is free once block k - kShaSlots is in
-                    // the round wave's registers.
-                    while (k >= (uint64_t) kShaSlots && budget > 0 &&
-                           __builtin_amdgcn_readfirstlane(__hip_atomic_load(&consumed, __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) <
-                               (uint32_t) (k - kShaSlots + 1)) {
-                        --budget;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    produce(k, nx[u]);
-                    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the rows are in LDS before the flag
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    __hip_atomic_store(&ready[k % kShaSlots], (uint32_t) (k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-        }
-#elif defined(CIO_SHA1_PREFETCH)
-        // Blocks 0..j+1 are written before barrier j (j = 0..wmax: wmax + 1
-        // barriers, as on the round wave); unrolled so each ring slot is a
-        // fixed register set.
-        for (uint64_t jb = 0; jb <= wmax + 1; jb += kShaAhead) {
-#pragma unroll
-            for (int u = 0; u < kShaAhead; ++u) {
-                if (jb + u <= wmax + 1) {
-                    produce(jb + u, nx[u]);
-                    if (jb + u >= 1) {
+                if (jb + (uint64_t) u * kShaSched < ngroups * kShaPer) {
+                    produce(jb + sw + (uint64_t) u * kShaSched, nx[u]);
+                    if ((u * kShaSched) % kShaPer == kShaPer - kShaSched) {
                         __syncthreads();
                     }
                 }
             }
         }
-#else
-        // Blocks [g kShaPer, (g + 1) kShaPer) are written before barrier g, one
-        // barrier per group as on the round wave; unrolled so each ring slot is
-        // a fixed register set.
-        const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
-        for (uint64_t jb = 0; jb < ngroups * kShaPer; jb += kShaAhead) {
-#pragma unroll
-            for (int u = 0; u < kShaAhead; ++u) {
-                if (jb + u < ngroups * kShaPer) {
-                    produce(jb + u, nx[u]);
-                    if (u % kShaPer == kShaPer - 1) {
-                        __syncthreads();
-                    }
-                }
-            }
-        }
-#endif
         return;
     }
 
     Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
-#if defined(CIO_SHA1_FLAGS)
-    // Block j + 1's flag and rows are read before block j's rounds run, so by
-    // the time they are checked they have landed; LDS serves one wave's
-    // operations in order, so rows read after a flag that says "ready" are the
-    // rows written before it.  A flag read too early is re-read (spin) with
-    // the rows after it.
-    uint4 ra[kShaRowsPerBlock], rb[kShaRowsPerBlock];
-    const uint4 *slot0 = &kw[0][0][lane];
-    constexpr uint32_t kSlotWords = kShaRowsPerBlock * 64;
-    auto fetch = [&](uint64_t k, uint4 (&rows)[kShaRowsPerBlock]) -> uint32_t {
-        const uint32_t f = __hip_atomic_load(&ready[k % kShaSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        sha1_load_rows(rows, slot0 + (uint32_t) (k % kShaSlots) * kSlotWords);
-        return f;
-    };
-    auto settle = [&](uint64_t k, uint32_t f, uint4 (&rows)[kShaRowsPerBlock]) {
-        while (__builtin_amdgcn_readfirstlane(f) != (uint32_t) (k + 1) && budget > 0) {
-            --budget;
-            __builtin_amdgcn_s_sleep(1);
-            f = fetch(k, rows);
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __hip_atomic_store(&consumed, (uint32_t) (k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // The rows were requested a whole block of rounds ago and have landed;
-        // saying so keeps the compiler from waiting on the next prefetch
-        // inside the next block's rounds.
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-    };
-    {
-        const uint32_t f0 = fetch(0, ra);
-        settle(0, f0, ra);
-    }
-    for (uint64_t j = 0; j < wmax; j += 2) {
-        const bool more = j + 1 < wmax;
-        uint32_t fb = 0;
-        if (more) {
-            fb = fetch(j + 1, rb);
-        }
-        if (j < nblk) {
-            sha1_block_rounds(st, ra);
-        }
-        if (!more) {
-            break;
-        }
-        settle(j + 1, fb, rb);
-        const bool more2 = j + 2 < wmax;
-        uint32_t fa = 0;
-        if (more2) {
-            fa = fetch(j + 2, ra);
-        }
-        if (j + 1 < nblk) {
-            sha1_block_rounds(st, rb);
-        }
-        if (more2) {
-            settle(j + 2, fa, ra);
-        }
-    }
-#elif defined(CIO_SHA1_PREFETCH)
-    // Ping-pong register sets (no 80-register copies): block j's rows were
-    // read before barrier j; block j + 1's go out before block j's rounds.
-    uint4 ra[kShaRowsPerBlock], rb[kShaRowsPerBlock];
-    const uint4 *slot0 = &kw[0][0][lane];
-    constexpr uint32_t kSlotWords = kShaRowsPerBlock * 64;   // uint4s per slot
-    uint32_t s1 = kSlotWords, s2 = 2 * kSlotWords;          // slots of blocks j + 1, j + 2
-    __syncthreads();                                   // barrier 0: blocks 0, 1
-    sha1_load_rows(ra, slot0);
-    __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0): no load of ra left in flight at the loop head
-    for (uint64_t j = 0; j < wmax; j += 2) {
-        sha1_load_rows(rb, slot0 + s1);
-        if (j < nblk) {
-            sha1_block_rounds(st, ra);
-        }
-        __syncthreads();                               // barrier j + 1
-        if (j + 1 < wmax) {
-            sha1_load_rows(ra, slot0 + s2);
-            if (j + 1 < nblk) {
-                sha1_block_rounds(st, rb);
-            }
-            __syncthreads();                           // barrier j + 2
-        }
-        // Slots advance by two blocks: (s1, s2) <- (s1 + 2, s2 + 2) mod 3 slots.
-        const uint32_t s0 = 3 * kSlotWords - s1 - s2;
-        s1 = s0;
-        s2 = s1 == 2 * kSlotWords ? 0u : s1 + kSlotWords;
-    }
-#else
-    const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
     for (uint64_t g = 0; g < ngroups; ++g) {
         __syncthreads();
         // All 20 rows of every block of the group are requested up front
-        // (80 VGPRs per block; this wave is alone on its SIMD), so the LDS
-        // latency after the barrier is paid once per group.
+        // (80 VGPRs per block), so the LDS latency after the barrier is paid
+        // once per group.
         uint4 rows[kShaPer][kShaRowsPerBlock];
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
@@ -440,23 +279,16 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         }
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
-#ifdef CIO_SHA1_SELECT
-            // Every lane runs the rounds (a wave issues them anyway) and lanes
-            // past their last block keep their state: no branch for the
-            // compiler to sink the row reads into.
-            Sha1State nx = st;
-            sha1_block_rounds(nx, rows[u]);
+            // Every lane runs the rounds (the wave issues them anyway) and a
+            // lane past its last block keeps its state: no branch for the
+            // compiler to sink the row reads into, so they stay in order.
+            Sha1State nxs = st;
+            sha1_block_rounds(nxs, rows[u]);
             const bool take = g * kShaPer + u < nblk;
-            st.h0 = take ? nx.h0 : st.h0; st.h1 = take ? nx.h1 : st.h1; st.h2 = take ? nx.h2 : st.h2;
-            st.h3 = take ? nx.h3 : st.h3; st.h4 = take ? nx.h4 : st.h4;
-#else
-            if (g * kShaPer + u < nblk) {
-                sha1_block_rounds(st, rows[u]);
-            }
-#endif
+            st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
+            st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
         }
     }
-#endif
     if (!live) {
         return;
     }
@@ -481,7 +313,7 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
     if (n > 0xFFFFFFFFull - 63) {
         return cioa_fail_msg("cio_sha1_batch_dev", "too many chunks for one launch");
     }
-    hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(128), 0, s,
+    hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(kShaThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), dev_offs, dev_lens, dev_digests, (uint32_t) n);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev: launch", hipGetErrorString(e));
