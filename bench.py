@@ -138,15 +138,20 @@ def geometry(cfg, rank, world):
     raise ValueError(cfg)
 
 
-def load_pmc_traffic(cfg):
-    """HBM bytes per launch of the main kernel from a committed rocprofv3 --pmc pass."""
+def load_pmc_traffic(cfg, bytes_per_launch):
+    """HBM bytes per launch of the main kernel, from a committed rocprofv3 --pmc
+    pass: the pass's measured traffic when it profiled launches of this size,
+    else its traffic/algorithmic ratio applied to this launch's bytes (a strong-
+    scaled shard at N > 1 launches fewer bytes than the N = 1 pass did)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        if d.get("algorithmic_bytes_per_launch") == bytes_per_launch:
+            return d.get("hbm_bytes_per_launch")
+        return int(round(d["traffic_over_algorithmic"] * bytes_per_launch))
     except Exception:
         return None
 
@@ -401,11 +406,12 @@ def run_crc(args, rank, world, device, dist):
                    "rotating_batches": nrot},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": load_pmc_traffic(args.config),
+                     "traffic": load_pmc_traffic(args.config, bytes_rank),
                      "traffic_source": (f"profiles/pmc_{args.config}.json: HBM bytes per launch of this kernel "
                                         "from a committed rocprofv3 --pmc pass (FETCH_SIZE x2 gfx950 "
-                                        "correction + WRITE_SIZE, separate passes); not measured in this run")
-                     if load_pmc_traffic(args.config) is not None else None,
+                                        "correction + WRITE_SIZE, separate passes; its traffic/algorithmic "
+                                        "ratio when this launch's size differs); not measured in this run")
+                     if load_pmc_traffic(args.config, bytes_rank) is not None else None,
                      "kernel": plan.kernel_name(), "kernel_ms_mean": round(kernel_ms, 5),
                      "timing": "HIP event pair on the launch stream around the K back-to-back timed "
                                "launches, divided by K (launch gaps included)",
