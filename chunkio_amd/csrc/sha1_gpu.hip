@@ -327,6 +327,9 @@ extern "C" int cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *de
     if (n == 0) {
         return CIO_OK;
     }
+    if (dev_base == nullptr || dev_offs == nullptr || dev_lens == nullptr || dev_digests == nullptr) {
+        return cioa_fail_msg("cio_sha1_batch_dev_async", "null pointer");
+    }
     if (cio_gpu_init() != CIO_OK) {
         return CIO_ERROR;
     }
@@ -338,6 +341,9 @@ extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, co
 {
     if (n == 0) {
         return CIO_OK;
+    }
+    if (dev_base == nullptr || offs == nullptr || lens == nullptr || dev_digests == nullptr) {
+        return cioa_fail_msg("cio_sha1_batch_dev", "null pointer");
     }
     if (cio_gpu_init() != CIO_OK) {
         return CIO_ERROR;

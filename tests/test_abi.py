@@ -80,3 +80,16 @@ def test_shift_and_combine_match_oracle():
     b = rng.integers(0, 256, 777, dtype=np.uint8)
     whole = po.crc_update(INIT, np.concatenate([a, b]))
     assert chunkio_amd.crc32_combine(po.crc_update(INIT, a), po.crc_update(0, b), len(b)) == whole
+
+
+def test_sha1_entry_points_reject_null_pointers_without_a_gpu():
+    """Argument checks run before any device call: a null descriptor or output
+    pointer is CIO_ERROR with a message, not a fault (no GPU needed)."""
+    lib = chunkio_amd.lib()
+    buf = ctypes.create_string_buffer(64)
+    assert lib.cio_sha1_batch_dev_async(None, None, None, None, 0, None) == 0   # empty batch: nothing to do
+    assert lib.cio_sha1_batch_dev_async(buf, None, buf, buf, 1, None) == -1
+    assert b"null pointer" in lib.cio_gpu_last_error()
+    offs = (ctypes.c_uint64 * 1)(0)
+    assert lib.cio_sha1_batch_dev(buf, offs, offs, None, 1, None) == -1
+    assert b"null pointer" in lib.cio_gpu_last_error()
