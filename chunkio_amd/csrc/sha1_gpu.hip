@@ -263,12 +263,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     }
 
     Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
-    for (uint64_t g = 0; g < ngroups; ++g) {
-        __syncthreads();
-        // All 20 rows of every block of the group are requested up front
-        // (80 VGPRs per block), so the LDS latency after the barrier is paid
-        // once per group.
-        uint4 rows[kShaPer][kShaRowsPerBlock];
+    auto load_group = [&](uint64_t g, uint4 (&rows)[kShaPer][kShaRowsPerBlock]) {
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
             const uint4 *row = &kw[(g * kShaPer + u) % kShaSlots][0][lane];
@@ -277,6 +272,8 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 rows[u][r] = row[r * 64];
             }
         }
+    };
+    auto run_group = [&](uint64_t g, const uint4 (&rows)[kShaPer][kShaRowsPerBlock]) {
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
             // Every lane runs the rounds (the wave issues them anyway) and a
@@ -288,6 +285,15 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
             st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
         }
+    };
+    for (uint64_t g = 0; g < ngroups; ++g) {
+        __syncthreads();
+        // All 20 rows of every block of the group are requested up front
+        // (80 VGPRs per block), so the LDS latency after the barrier is paid
+        // once per group.
+        uint4 rows[kShaPer][kShaRowsPerBlock];
+        load_group(g, rows);
+        run_group(g, rows);
     }
     if (!live) {
         return;
