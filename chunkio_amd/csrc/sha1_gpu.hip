@@ -145,12 +145,13 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
 // schedule wave needed more than that per block (~250 instructions plus its
 // LDS writes: a build whose round wave did no rounds took 4.5 ms per cfg5
 // batch), so it, not the chain, set the pace; two schedule waves halve it.
-// Blocks are handed over kShaPer at a time through 2 kShaPer LDS slots, one
-// barrier per group (a barrier per block cost ~3 cycles per round).
+// Blocks are handed over kShaPer (4) at a time through 2 kShaPer LDS slots
+// (160 KiB), one barrier per group (a barrier per block cost ~3 cycles per
+// round).
 #ifdef CIO_SHA1_GROUP
 constexpr int kShaPer = CIO_SHA1_GROUP;           // blocks handed over per barrier
 #else
-constexpr int kShaPer = 2;
+constexpr int kShaPer = 4;
 #endif
 #ifdef CIO_SHA1_SCHED_WAVES
 constexpr int kShaSched = CIO_SHA1_SCHED_WAVES;   // schedule waves
@@ -288,11 +289,14 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     };
     for (uint64_t g = 0; g < ngroups; ++g) {
         __syncthreads();
-        // All 20 rows of every block of the group are requested up front
-        // (80 VGPRs per block), so the LDS latency after the barrier is paid
-        // once per group.
+        // All 20 rows of every block of the group are requested up front, so
+        // the LDS latency after the barrier is paid once per group.
         uint4 rows[kShaPer][kShaRowsPerBlock];
         load_group(g, rows);
+        // Every row lands before the rounds start: LDS data arriving while the
+        // round chain issues slows the chain more than the wait costs
+        // (profiles/r02/sha1/sha1_ab_wait.txt, sha1_ab_ahead.txt).
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
         run_group(g, rows);
     }
     if (!live) {
