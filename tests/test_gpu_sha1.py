@@ -81,3 +81,22 @@ def test_async_device_descriptors(cuda, golden):
     host = rdev.cpu().numpy()
     for i in range(len(rl)):
         assert bytes(got[i]) == hashlib.sha1(host[int(ro[i]):int(ro[i] + rl[i])].tobytes()).digest(), i
+
+
+def test_many_workgroups_ragged_and_misaligned(cuda):
+    """20,011 chunks (313 workgroups of 64 lanes, more than one per CU) with
+    lengths 0..3000 at arbitrary byte offsets: lanes of one wave end at
+    different blocks and most take the byte-wise message path."""
+    import torch
+    rng = np.random.default_rng(23)
+    n = 20011
+    lens = rng.integers(0, 3001, n).astype(np.uint64)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 16, n - 1).astype(np.uint64))
+    total = int(offs[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    dev = torch.from_numpy(host).to(cuda)
+    got = cio.sha1_batch_dev(dev, offs, lens)
+    for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
