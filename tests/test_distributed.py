@@ -138,3 +138,20 @@ def test_bench_gpus_n_spawns_ranks_or_refuses(tmp_path):
     assert r.returncode == 2, r.stderr
     assert "--gpus 2 but only 0 GPU(s) visible" in r.stderr
     assert r.stdout == ""
+
+
+def test_bench_traffic_scales_to_a_shards_launch():
+    """roofline.traffic at N > 1: a strong-scaled cfg4 shard launches 1/N of the
+    bytes the committed N = 1 PMC pass profiled, so the bench applies that
+    pass's traffic/algorithmic ratio instead of its absolute bytes."""
+    import json
+    import bench
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           "profiles", "pmc_cfg4.json")) as f:
+        d = json.load(f)
+    full = d["algorithmic_bytes_per_launch"]
+    assert bench.load_pmc_traffic("cfg4", full) == d["hbm_bytes_per_launch"]
+    for world in (2, 4, 8):
+        got = bench.load_pmc_traffic("cfg4", full // world)
+        assert got == round(d["traffic_over_algorithmic"] * (full // world))
+    assert bench.load_pmc_traffic("no_such_config", 1) is None
