@@ -280,6 +280,8 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             // Every lane runs the rounds (the wave issues them anyway) and a
             // lane past its last block keeps its state: no branch for the
             // compiler to sink the row reads into, so they stay in order.
+            // (A per-lane branch instead measured 5% slower: the compiler
+            // then spilled rows to AGPRs, sha1_ab_branch.txt.)
             Sha1State nxs = st;
             sha1_block_rounds(nxs, rows[u]);
             const bool take = g * kShaPer + u < nblk;
