@@ -596,6 +596,10 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
             }
         };
         if (direct) {
+            // The data DMA needs no plan: queue it first and build the plan
+            // while the engine moves the group (the plan only has to precede
+            // the metadata copy and the kernel on this stream).
+            if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
             build();
         } else {
             // staged: the plan is built while the copy workers fill the slot
@@ -614,9 +618,7 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
             break;
         }
         if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
-        if (direct) {
-            if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
-        } else {
+        if (!direct) {
             if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
         }
         if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
