@@ -1479,7 +1479,8 @@ const char *cio_gpu_version(void)
 {
     return "chunkio_amd crc32 v8 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains division-free-start "
            "slice4-lds32x perm horner-fold direct-whole preshifted-partials wg-lds-fold) small(dpp-reduce bitop3-fold) "
-           "host(nt-staging graduated-groups pread-bounce multi-device)";
+           "host(nt-staging graduated-groups pread-bounce multi-device) "
+           "sha1(2-schedule-waves 4-block-handover)";
 }
 
 int cio_gpu_init(void)
