@@ -479,7 +479,11 @@ def run_sha1(args, rank, world, device, dist):
             "config": {**desc, "workload": "cfg5: SHA-1 over 1024 x 409600 B per GPU"},
             "roofline": {"bound": "valu-latency", "achieved": round(value / world, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(value / world / HBM_PEAK_GBS, 5), "traffic": None},
+                         "frac": round(value / world / HBM_PEAK_GBS, 5),
+                         "traffic": load_pmc_traffic("sha1", int(lens.sum())),
+                         "traffic_source": "profiles/pmc_sha1.json: HBM bytes per launch of sha1_kernel from a "
+                                           "committed rocprofv3 --pmc pass; not measured in this run"
+                         if load_pmc_traffic("sha1", int(lens.sum())) is not None else None},
             "timing": "K launches of cio_sha1_batch_dev_async (device-resident offsets/lengths) back to back, "
                       "host clock between stream syncs",
             "check": check}

@@ -12,6 +12,7 @@ for CFG in "$@"; do
     cfg3) ALGO=39748485057; STEPS=4; WARM=1 ;;
     cfg4) ALGO=34359738368; STEPS=4; WARM=1 ;;
     cfg4k) ALGO=419430400; STEPS=20; WARM=20 ;;
+    sha1) ALGO=419430400; STEPS=5; WARM=1 ;;
     *) ALGO=419430400; STEPS=20; WARM=20 ;;
   esac
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$CFG -o run --output-format csv -- \

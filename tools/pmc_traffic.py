@@ -16,8 +16,8 @@ import json
 import os
 import sys
 
-# the CRC kernel a bench config launches (one of the two per run)
-KERNELS = ("crc32_stream_kernel", "crc32_small_kernel")
+# the main kernel a bench config launches (one per run)
+KERNELS = ("crc32_stream_kernel", "crc32_small_kernel", "sha1_kernel")
 
 
 kern_seen = set()
