@@ -1194,9 +1194,15 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         chunk(rb, c + 1);
     }
 #else
+    // Issue priority rotates per chunk as in the stream kernel, so no wave of
+    // a SIMD stays behind its mates under the age tie-break (cfg4k 68.7 ->
+    // 66.6 us back to back, profiles/r02/ab_small_prio_rotation.txt).
+    const uint32_t slot_group = __builtin_amdgcn_readfirstlane((tid >> 6) >> 2);
     for (uint32_t c = c0; c < c1; ++c) {
+        rotate_prio(slot_group, c - c0);
         chunk(cur, c);
     }
+    __builtin_amdgcn_s_setprio(0);
 #endif
     tiny_chunks(lds, lb_lo, base, desc, tiny, seeds, out, nullptr, ntiny, wave, lane, W);
 }
@@ -1478,7 +1484,7 @@ const char *cio_gpu_last_error(void)
 const char *cio_gpu_version(void)
 {
     return "chunkio_amd crc32 v8 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains division-free-start "
-           "slice4-lds32x perm horner-fold direct-whole preshifted-partials wg-lds-fold) small(dpp-reduce bitop3-fold) "
+           "slice4-lds32x perm horner-fold direct-whole preshifted-partials wg-lds-fold) small(dpp-reduce bitop3-fold prio-rotate) "
            "host(nt-staging graduated-groups pread-bounce multi-device) "
            "sha1(2-schedule-waves 4-block-handover)";
 }
