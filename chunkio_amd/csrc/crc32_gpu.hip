@@ -1199,7 +1199,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     // 66.6 us back to back, profiles/r02/ab_small_prio_rotation.txt).
     const uint32_t slot_group = __builtin_amdgcn_readfirstlane((tid >> 6) >> 2);
     for (uint32_t c = c0; c < c1; ++c) {
-        rotate_prio(slot_group, c - c0);
+        rotate_prio(slot_group, c - c0);   // (reversed or every-2-chunks rotation: neutral)
         chunk(cur, c);
     }
     __builtin_amdgcn_s_setprio(0);
