@@ -14,8 +14,12 @@ Prints ONE JSON line (rank 0).  `value` = bytes of all ranks x K / wall time
 of the K timed launches (max over ranks).  `roofline.achieved` = algorithmic
 bytes per launch of the CRC kernel (sum of chunk lengths) / its average launch
 duration: one HIP event pair recorded on the launch stream around the K
-back-to-back timed launches, divided by K (inter-kernel gaps included, so it
-is >= rocprofv3 --kernel-trace's average kernel duration).  Launches bracketed
+back-to-back timed launches, divided by K.  That average includes the short
+GPU-side gaps between back-to-back kernels, but it is NOT an upper bound on
+rocprofv3 --kernel-trace's per-dispatch mean: under the profiler every
+dispatch carries its own completion signal and runs ~0.3-2 % longer, so the
+two agree to within ~2 % either way (profiles/r03/README.md pairs them run
+by run).  Launches bracketed
 one by one with their own events (perturbed: the event packets serialise the
 queue) are reported after the timed region as `isolated_launch_ms`.  `roofline.read_stream` is the
 same-box ceiling for the access pattern: a read-only kernel with the CRC
@@ -69,11 +73,12 @@ def dist_setup(args):
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        # The data path has no collective (chunks shard round-robin), so no
+        # RCCL communicator is created at all: the contract's barrier and the
+        # two scalar reductions (max-over-ranks, per-GPU gather) run on gloo
+        # over CPU tensors, for every N.
         import torch.distributed as dist
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     if args.gpus != world:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     return rank, world, torch.device("cuda", local), dist
@@ -85,24 +90,22 @@ def barrier(dist):
 
 
 def max_over_ranks(x, dist, device):
+    """MAX of a host scalar over ranks (gloo, CPU tensor)."""
     if dist is None:
         return x
     import torch
-    on_cpu = dist.get_backend() == "gloo"
-    t = torch.tensor([x], dtype=torch.float64, device="cpu" if on_cpu else device)
+    t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def gather_over_ranks(x, dist, device):
-    """[x of rank 0, x of rank 1, ...] (every rank gets the list)."""
+    """[x of rank 0, x of rank 1, ...] (every rank gets the list; gloo, CPU)."""
     if dist is None:
         return [x]
     import torch
-    on_cpu = dist.get_backend() == "gloo"
-    dev = "cpu" if on_cpu else device
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    out = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(dist.get_world_size())]
+    t = torch.tensor([x], dtype=torch.float64)
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [float(v.item()) for v in out]
 
@@ -504,6 +507,7 @@ def run_e2e(args, rank, world, device, dist):
     barrier(dist)
     elapsed = max_over_ranks(time.perf_counter() - t0, dist, device)
     value = int(lens.sum()) * world * steps / elapsed / 1e9
+    legs_staged = cio.pipe_last_timing()
     # Same batch with the host buffer pinned in place once (long-lived chunk
     # mappings): the pipeline DMAs it directly, no staging copy.
     treg = time.perf_counter()
@@ -518,6 +522,7 @@ def run_e2e(args, rank, world, device, dist):
             out_reg = cio.crc32_batch_host_packed(host, offs, lens)
         barrier(dist)
         elapsed_reg = max_over_ranks(time.perf_counter() - t0, dist, device)
+        legs_reg = cio.pipe_last_timing()
     finally:
         cio.host_unregister(host)
     value_reg = int(lens.sum()) * world * steps / elapsed_reg / 1e9
@@ -538,7 +543,15 @@ def run_e2e(args, rank, world, device, dist):
                                     "register_ms_once": round(reg_ms, 2),
                                     "note": "host batch pinned once with cio_crc32_host_register "
                                             "(outside the timed loop); chunks DMA'd directly"},
-            "breakdown": e2e_breakdown(host, device), "check": check}
+            "breakdown": e2e_breakdown(host, device),
+            "pipe_legs_last_call": {"staged": legs_staged, "registered": legs_reg,
+                                    "note": "cio_gpu_pipe_last_timing() after the last timed call: total = the "
+                                            "library's wall time for the batch; copy = host copy into pinned "
+                                            "staging (caller's view, overlapped with the DMA of earlier "
+                                            "groups); slot_wait = waiting for a staging slot to drain; "
+                                            "total minus the DMA bound (bytes / pinned_h2d_GBps) is "
+                                            "pipeline fill/drain and host overhead"},
+            "check": check}
 
 
 def e2e_breakdown(host, device):
@@ -564,7 +577,7 @@ def e2e_breakdown(host, device):
             "torch_threads": torch.get_num_threads()}
 
 
-def run_perf(args, rank, world, device, dist):
+def run_perf(args, rank, world, device, dist, compact=False):
     """BASELINE config 1's loop (`tools/cio -k -p 400kb.txt`: 1000 files x 5 x
     409600 B with CRC32) through the C chunk layer (cioa_bench_perf_write,
     include/chunkio_amd/cioa_chunk.h): appends only copy (CIOA_DEFERRED_CRC)
@@ -580,6 +593,10 @@ def run_perf(args, rank, world, device, dist):
     d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8).tobytes()
     files, writes, batch = 1000, 5, 100
     reps = max(1, min(args.steps, 3))
+    if compact:
+        # the default line's leg: the deferred C layer only, one warm pass +
+        # `reps` timed; the reference loop is cpu_baseline.cio_perf_k_p there
+        reps = max(1, min(args.steps, 2))
 
     def timed(flags, tag):
         times = []
@@ -599,6 +616,19 @@ def run_perf(args, rank, world, device, dist):
         return min(times), nb, hdr_ok
 
     t_def, nbytes, ok_def = timed(cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, "deferred")
+    if compact:
+        return {"metric": "cio -k -p loop (1000 files x 5 x 400 KB, CRC32) GB/s with deferred CRC + batched "
+                          "GPU sync", "value": round(nbytes / t_def / 1e9, 3), "unit": "GB/s", "steps": reps,
+                "warmup": 1, "ms_per_step": round(t_def * 1e3, 2), "scaling": "weak",
+                "vs_baseline": round(nbytes / t_def / 545_507_660, 2),
+                "vs_baseline_note": "BASELINE.md's published `cio -k -p` rate, 545,507,660 B/s (README.md:120-129, "
+                                    "hardware unstated)",
+                "config": {"workload": "config 1 loop through the C chunk layer (cioa_bench_perf_write): open, "
+                                       "5 x write 409600 B, sync (batches of 100 chunks per GPU pass), close",
+                           "files": files, "writes": writes, "sync_batch": batch},
+                "check": {"last_file_header_c100088740e7": bool(ok_def)},
+                "cpu_baseline_ref": "cpu_baseline.cio_perf_k_p of this line: the reference loop with the "
+                                    "reference's own crc_update, same box, same run"}
     t_imm, _, ok_imm = timed(cf.CIO_CHECKSUM, "immediate")
     from oracle import pyoracle as po
     lib = po.ref()
@@ -633,7 +663,7 @@ def run_perf(args, rank, world, device, dist):
                              "crc_off_GBps": ref["crc_off"]["GBps"], **cpu_info()}}
 
 
-def run_verify(args, rank, world, device, dist):
+def run_verify(args, rank, world, device, dist, compact=False):
     """batched verify-on-load of a stream directory.  1000
     chunk files as `tools/cio -k -p` leaves them (2,068,480 B each: header,
     5 x 400kb.txt, CRC 0x088740E7; one of them with a flipped content byte)
@@ -648,6 +678,7 @@ def run_verify(args, rank, world, device, dist):
     d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8).tobytes()
     files, bad = 1000, 500
     reps = max(1, min(args.steps, 10))
+    ncpu = 100 if compact else 200
     root = tempfile.mkdtemp(prefix="cioa-verify-")
     try:
         paths = [os.path.join(root, f"perf-test-{i:04d}.txt") for i in range(files)]
@@ -686,7 +717,6 @@ def run_verify(args, rank, world, device, dist):
             if lib is None:
                 lib, kind, fn = po.oracle(), "port", "oracle_crc_update"
             f_upd = getattr(lib, fn)
-            ncpu = 200
             t0 = time.perf_counter()
             nbad = 0
             for p in paths[:ncpu]:
@@ -795,15 +825,43 @@ def free_port():
         return so.getsockname()[1]
 
 
+def visible_gpus():
+    """GPUs this process could use, counted WITHOUT touching the GPU: the KFD
+    topology in sysfs (nodes with SIMDs) whose DRM render node this process
+    may open (a container can list every GPU of the host in sysfs but hold
+    only some render nodes), narrowed by the *_VISIBLE_DEVICES lists the
+    runtime honours.  Returns (count, how)."""
+    import glob
+    n = 0
+    for prop in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(prop) as f:
+                kv = dict(line.split(None, 1) for line in f if line.strip())
+        except (OSError, ValueError):
+            continue
+        if int(kv.get("simd_count", "0")) <= 0:
+            continue
+        minor = kv.get("drm_render_minor", "").strip()
+        if minor and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            continue
+        n += 1
+    how = "kfd-sysfs+render-node-access"
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+            how += f"+{var}"
+    return n, how
+
+
 def spawn_ranks(args):
     """`python bench.py --gpus N` with no launcher environment: start N rank
     processes of this script (one per GPU, the layout torch.distributed.run
     gives) and exit with the worst child status.  Nothing here touches the GPU
-    (device_count() does not initialise it on this image), so the children
-    start from a clean process."""
+    (the devices are counted from sysfs, torch is not imported), so the
+    children start from a clean process."""
     import subprocess
-    import torch
-    visible = torch.cuda.device_count()
+    visible, _ = visible_gpus()
     rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1"
     if visible < args.gpus and not rehearse:
         print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
@@ -829,20 +887,32 @@ def other_configs(args, rank, world, device, dist):
     import torch
     out = {}
     t0 = time.perf_counter()
-    for cfg, steps, warm in (("cfg3", 5, 2), ("sha1", 10, 2), ("e2e", 30, 10)):
+    legs = [("cfg3", 5, 2), ("sha1", 10, 2), ("e2e", 30, 10)]
+    if world == 1:
+        # SURVEY §8(f) rows 1 and 3 (host-side, one process): batched
+        # verify-on-load of 1000 chunk files, and the config-1 loop through
+        # the C chunk layer with deferred CRC + batched GPU sync.
+        legs += [("verify", 3, 1), ("perf", 2, 1)]
+    for cfg, steps, warm in legs:
         torch.cuda.empty_cache()
         a = copy.copy(args)
-        a.config, a.steps, a.warmup, a.no_cpu = cfg, steps, warm, True
+        a.config, a.steps, a.warmup = cfg, steps, warm
+        a.no_cpu = cfg != "verify" or args.no_cpu
         t1 = time.perf_counter()
         if cfg == "sha1":
             r = run_sha1(a, rank, world, device, dist)
         elif cfg == "e2e":
             r = run_e2e(a, rank, world, device, dist)
+        elif cfg == "verify":
+            r = run_verify(a, rank, world, device, dist, compact=True)
+        elif cfg == "perf":
+            r = run_perf(a, rank, world, device, dist, compact=True)
         else:
             r = run_crc(a, rank, world, device, dist)
         keep = {k: r[k] for k in ("metric", "value", "unit", "scaling", "steps", "warmup", "ms_per_step")}
         keep["workload"] = r["config"].get("workload")
-        for k in ("roofline", "check", "per_gpu", "registered_in_place", "breakdown"):
+        for k in ("roofline", "check", "per_gpu", "registered_in_place", "breakdown", "pipe_legs_last_call",
+                  "cpu_baseline", "cpu_baseline_ref", "vs_baseline", "vs_baseline_note"):
             if k in r:
                 keep[k] = r[k]
         if "roofline" in keep:

@@ -21,8 +21,10 @@ EXPORTS = (
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_batch_dev", "cio_crc32_batch_host",
     "cio_crc32_batch_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device",
-    "cio_crc32_host_register", "cio_crc32_host_unregister",
-    "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_sha1_batch_dev_async", "cio_gpu_read_stream",
+    "cio_crc32_host_register", "cio_crc32_host_unregister", "cio_gpu_pipe_last_timing",
+    "cio_crc32_cpu_max", "cio_crc32_set_cpu_max",
+    "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_sha1_batch_dev_async",
+    "cio_sha1_state_init", "cio_sha1_update_batch_dev", "cio_sha1_final_batch_dev", "cio_gpu_read_stream",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
     # include/chunkio_amd/cio_verify.h
@@ -74,10 +76,16 @@ def _bind(lib):
         "cio_gpu_get_device": (ctypes.c_int, []),
         "cio_crc32_host_register": (ctypes.c_int, [V, ctypes.c_size_t]),
         "cio_crc32_host_unregister": (ctypes.c_int, [V]),
+        "cio_gpu_pipe_last_timing": (ctypes.c_int, [P(ctypes.c_double), ctypes.c_int]),
+        "cio_crc32_cpu_max": (ctypes.c_size_t, []),
+        "cio_crc32_set_cpu_max": (None, [ctypes.c_size_t]),
         "cio_gpu_fill_synthetic": (ctypes.c_int, [V, c_u64_p, c_u64_p, c_u64_p, ctypes.c_size_t,
                                                   ctypes.c_uint64, V]),
         "cio_sha1_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, ctypes.c_size_t, V]),
         "cio_sha1_batch_dev_async": (ctypes.c_int, [V, V, V, V, ctypes.c_size_t, V]),
+        "cio_sha1_state_init": (None, [V, ctypes.c_size_t]),
+        "cio_sha1_update_batch_dev": (ctypes.c_int, [V, V, V, V, ctypes.c_size_t, V]),
+        "cio_sha1_final_batch_dev": (ctypes.c_int, [V, V, ctypes.c_size_t, V]),
         "cio_gpu_read_stream": (ctypes.c_int, [V, ctypes.c_uint64, V]),
         "cio_gpu_event_create": (V, []),
         "cio_gpu_event_destroy": (None, [V]),

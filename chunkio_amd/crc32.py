@@ -212,6 +212,14 @@ def device_count():
     return int(_lib.lib().cio_gpu_device_count())
 
 
+def pipe_last_timing():
+    """Host legs of the last host/file batch (cio_gpu_pipe_last_timing), ms."""
+    v = (ctypes.c_double * 6)()
+    _lib.check(_lib.lib().cio_gpu_pipe_last_timing(v, 6), "cio_gpu_pipe_last_timing")
+    return {"total_ms": round(v[0], 3), "copy_ms": round(v[1], 3), "slot_wait_ms": round(v[2], 3),
+            "plan_ms": round(v[3], 3), "groups": int(v[4]), "staged_bytes": int(v[5])}
+
+
 def host_register(arr):
     """Pin a long-lived host buffer (numpy array / mmap view) in place so that
     crc32_batch_host DMAs chunks inside it directly (no staging copy)."""
@@ -262,3 +270,43 @@ def sha1_batch_dev_async(base, dev_offs, dev_lens, dev_digests, stream=None):
     _lib.check(_lib.lib().cio_sha1_batch_dev_async(_ptr(base), _ptr(dev_offs), _ptr(dev_lens), _ptr(dev_digests),
                                                    n, _stream_ptr(stream)),
                "cio_sha1_batch_dev_async")
+
+
+SHA1_STATE_BYTES = 96     # sizeof(cio_sha1_state): h[5], num, total, block[64]
+
+
+def sha1_states_init(n, device):
+    """n fresh SHA-1 contexts (SHA1_Init, cio_sha1_state_init) as a uint8
+    device tensor of n x 96 bytes."""
+    import torch
+    host = np.zeros(max(n, 1) * SHA1_STATE_BYTES, dtype=np.uint8)
+    _lib.lib().cio_sha1_state_init(host.ctypes.data, n)
+    return torch.from_numpy(host[: n * SHA1_STATE_BYTES].copy()).to(device)
+
+
+def sha1_states_view(states):
+    """Host view of device SHA-1 contexts: dict of numpy arrays h (n x 5),
+    num (n), total (n), block (n x 64)."""
+    raw = states.cpu().numpy().reshape(-1, SHA1_STATE_BYTES)
+    return {"h": raw[:, :20].copy().view("<u4"), "num": raw[:, 20:24].copy().view("<u4")[:, 0],
+            "total": raw[:, 24:32].copy().view("<u8")[:, 0], "block": raw[:, 32:].copy()}
+
+
+def sha1_update_batch_dev(base, dev_offs, dev_lens, states, stream=None):
+    """SHA1_Update of chunk i (device tensors dev_offs/dev_lens, int64) into
+    context i of `states` (sha1_states_init); one launch, no sync."""
+    n = int(dev_offs.numel())
+    assert dev_lens.numel() == n and states.numel() >= SHA1_STATE_BYTES * n
+    _lib.check(_lib.lib().cio_sha1_update_batch_dev(_ptr(base), _ptr(dev_offs), _ptr(dev_lens), _ptr(states), n,
+                                                    _stream_ptr(stream)),
+               "cio_sha1_update_batch_dev")
+
+
+def sha1_final_batch_dev(states, n=None, stream=None):
+    """SHA1_Final of every context (left unchanged): n x 20 digest bytes (numpy)."""
+    import torch
+    n = states.numel() // SHA1_STATE_BYTES if n is None else n
+    out = torch.empty(max(n, 1) * 20, dtype=torch.uint8, device=states.device)
+    _lib.check(_lib.lib().cio_sha1_final_batch_dev(_ptr(states), _ptr(out), n, _stream_ptr(stream)),
+               "cio_sha1_final_batch_dev")
+    return out[: n * 20].cpu().numpy().reshape(n, 20)

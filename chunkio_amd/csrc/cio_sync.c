@@ -17,6 +17,7 @@
 #include "chunkio_amd/cio_verify.h"
 #include "chunkio_amd/cio_sync.h"
 #include "cio_layout.h"
+#include "crc32_host.h"
 
 int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev)
 {
@@ -62,7 +63,7 @@ int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags, const i
         it->crc_end = end;      /* committed below, after the batch ran */
         m++;
     }
-    if (m > 0 && cio_crc32_batch_host_multi(bufs, lens, seeds, raw, m, devices, ndev) != CIO_OK) {
+    if (m > 0 && cioa_crc_batch_route(bufs, lens, seeds, raw, m, devices, ndev) != CIO_OK) {
         /* restore the ranges: nothing was written */
         for (size_t k = 0; k < m; k++) {
             items[idx[k]].crc_end = (uint64_t) ((const unsigned char *) bufs[k] - items[idx[k]].map);

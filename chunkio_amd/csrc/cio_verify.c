@@ -6,7 +6,9 @@
  * order as the reference; then ONE GPU batch (spread over the caller's
  * devices) computes the CRC of every chunk that passed
  * (cio_crc32_batch_host_multi), and the 8-byte header compare runs on the
- * host.  No CRC is computed on the CPU here.
+ * host.  A batch whose regions total at most cio_crc32_cpu_max() bytes (one
+ * small chunk on open/up) is CRC'd by crc_update on this thread instead
+ * (crc_route.c: below the measured crossover a GPU round trip is slower).
  */
 #define _GNU_SOURCE
 #include <stdint.h>
@@ -26,6 +28,7 @@
 #include "chunkio_amd/cio_crc32_gpu.h"
 #include "chunkio_amd/cio_verify.h"
 #include "cio_layout.h"
+#include "crc32_host.h"
 
 int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags, const int *devices, int ndev)
 {
@@ -107,7 +110,7 @@ int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags, con
         }
     }
     if (m > 0) {
-        if (cio_crc32_batch_host_multi(bufs, lens, NULL, raw, m, devices, ndev) != CIO_OK) {
+        if (cioa_crc_batch_route(bufs, lens, NULL, raw, m, devices, ndev) != CIO_OK) {
             rc = CIO_ERROR;
             goto out;
         }
@@ -211,6 +214,17 @@ static void *check_slice(void *arg)
                 continue;
             }
             cioa_write_init_header(h, ck);
+            if (ck) {
+                /* This call closes the file itself, so it also does what the
+                 * reference's close does to a chunk prepared this way: the
+                 * chunk is unsynced (cio_file.c:396), munmap_file syncs it
+                 * (:317) and finalize_checksum stores htonl(crc_finalize(
+                 * crc_cur)) in the 8-byte field (:116-124, :1228), i.e.
+                 * 41 d9 12 ff 00 00 00 00 -- so the next verify passes. */
+                const uint32_t fin = htonl((uint32_t) crc_finalize((crc_t) CIOA_CRC_EMPTY_RAW));
+                memcpy(h + 2, &fin, 4);
+                memset(h + 6, 0, 4);
+            }
             if (posix_fallocate(j->fds[i], 0, j->page) != 0 ||
                 pwrite(j->fds[i], h, CIOA_HDR_MIN, 0) != CIOA_HDR_MIN) {
                 j->status[i] = CIO_ERROR;
@@ -355,7 +369,7 @@ int cio_verify_paths_multi(const char *const *paths, size_t n, int flags, const 
             bidx[m++] = i;
         }
     }
-    if (m > 0 && cio_crc32_batch_fd_multi(bfd, boff, blen, NULL, raw, m, devices, ndev) != CIO_OK) {
+    if (m > 0 && cioa_crc_fd_route(bfd, boff, blen, NULL, raw, m, devices, ndev) != CIO_OK) {
         rc = CIO_ERROR;
         proto.flags &= ~CIOA_VERIFY_DELETE_IRRECOVERABLE;     /* nothing is known to be irrecoverable */
     }

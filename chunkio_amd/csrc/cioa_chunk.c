@@ -42,6 +42,7 @@
 #include "chunkio_amd/cio_sync.h"
 #include "chunkio_amd/cioa_chunk.h"
 #include "cio_layout.h"
+#include "crc32_host.h"
 
 #define CIOA_REALLOC_HINT_MAX (8 * 1000 * 1000)   /* chunkio.h:60 */
 #define ROUND_UP(N, S) ((((N) + (S) - 1) / (S)) * (S))
@@ -266,7 +267,7 @@ static int calculate_checksum(cioa_chunk *ch, uint32_t *out)
     const void *buf = ch->map + CIOA_HDR_CONTENT_OFFSET;
     size_t len = 2 + (size_t) cioa_st_meta_len(ch->map) + (clen > 0 ? (size_t) clen : 0);
     uint32_t seed = ch->crc_cur;
-    return cio_crc32_batch_host_multi(&buf, &len, &seed, out, 1, ch->ctx->devs, ch->ctx->ndev);
+    return cioa_crc_batch_route(&buf, &len, &seed, out, 1, ch->ctx->devs, ch->ctx->ndev);
 }
 
 /* Does cio_file_calculate_checksum (cio_file.c:66-94) hash exactly the data
@@ -1353,54 +1354,80 @@ cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext
 
     cio_verify_item *items = calloc(n ? n : 1, sizeof(*items));
     size_t *vidx = calloc(n ? n : 1, sizeof(*vidx));
-    size_t m = 0, budget = ctx->max_up > ctx->total_up ? ctx->max_up - ctx->total_up : 0;
-    int vflags = 0;
-    for (size_t i = 0; i < n && items && vidx; i++) {
-        cioa_chunk *ch = chunk_new(ctx, st, ents[i].name, ctx->flags);
-        if (!ch) {
+    /* Rounds: up to the free max_chunks_up slots are opened, mapped and then
+     * verified in one batch.  The reference counts a chunk as up only once
+     * its format check passed (cio_file.c:490), so a chunk that fails frees
+     * its slot for the next file: the next round takes the files after the
+     * batch, until the slots or the files run out.  Files past the budget are
+     * registered down, unverified (cio_file.c:566). */
+    int verify_failed = 0;
+    size_t i = 0;
+    while (i < n && items && vidx) {
+        size_t m = 0, budget = ctx->max_up > ctx->total_up ? ctx->max_up - ctx->total_up : 0;
+        int vflags = 0;
+        for (; i < n; i++) {
+            if (budget == 0 && m > 0) {
+                break;                           /* verify these first: failures free slots */
+            }
+            cioa_chunk *ch = chunk_new(ctx, st, ents[i].name, ctx->flags);
+            if (!ch) {
+                continue;
+            }
+            ents[i].ch = ch;
+            if (budget == 0 || verify_failed) {                 /* registered down */
+                update_size(ch);
+                continue;
+            }
+            int fresh = 0, ret = native_open(ch);
+            if (ret == CIO_OK && update_size(ch) != CIO_OK) {
+                ret = CIO_ERROR;
+            }
+            if (ret == CIO_OK) {
+                ret = map_prepare(ch, ch->fs_size, &fresh);
+            }
+            if (ret != CIO_OK) {
+                ents[i].prepared = ret;                         /* failed before the CRC */
+                continue;
+            }
+            budget--;
+            if (fresh) {
+                ctx->total_up++;
+                ents[i].prepared = 2;
+                continue;
+            }
+            items[m].map = ch->map;
+            items[m].fs_size = ch->fs_size;
+            items[m].taint = 0;
+            vidx[m++] = i;
+            vflags = verify_flags(ch);
+            ents[i].prepared = 1;
+        }
+        if (m == 0) {
             continue;
         }
-        ents[i].ch = ch;
-        if (budget == 0) {                                   /* registered down */
-            update_size(ch);
-            continue;
+        const int vrc = cio_file_verify_batch_multi(items, m, vflags, ctx->devs, ctx->ndev);
+        for (size_t k = 0; k < m; k++) {
+            struct scan_ent *e = &ents[vidx[k]];
+            if (vrc != CIO_OK) {
+                /* The batch itself could not run (GPU failure): nothing is
+                 * known about these files, so they are registered down,
+                 * unverified, like the chunks past the budget -- a later
+                 * cioa_chunk_up verifies them -- and the scan reports the
+                 * failure through cioa_last_chunk_error() (CIO_ERROR). */
+                native_unmap(e->ch);
+                native_close(e->ch);
+                e->ch->data_size = 0;
+                e->prepared = 0;
+                continue;
+            }
+            e->prepared = map_finish(e->ch, &items[k]) == CIO_OK ? 2 : CIO_CORRUPTED;
         }
-        int fresh = 0, ret = native_open(ch);
-        if (ret == CIO_OK && update_size(ch) != CIO_OK) {
-            ret = CIO_ERROR;
-        }
-        if (ret == CIO_OK) {
-            ret = map_prepare(ch, ch->fs_size, &fresh);
-        }
-        if (ret != CIO_OK) {
-            ents[i].prepared = ret;                         /* failed before the CRC */
-            continue;
-        }
-        budget--;
-        if (fresh) {
-            ctx->total_up++;
-            ents[i].prepared = 2;
-            continue;
-        }
-        items[m].map = ch->map;
-        items[m].fs_size = ch->fs_size;
-        items[m].taint = 0;
-        vidx[m++] = i;
-        vflags = verify_flags(ch);
-        ents[i].prepared = 1;
-    }
-    int vrc = CIO_OK;
-    if (m > 0) {
-        vrc = cio_file_verify_batch_multi(items, m, vflags, ctx->devs, ctx->ndev);
-    }
-    for (size_t k = 0; k < m; k++) {
-        struct scan_ent *e = &ents[vidx[k]];
         if (vrc != CIO_OK) {
-            native_unmap(e->ch);
-            e->prepared = CIO_ERROR;
-            continue;
+            verify_failed = 1;
         }
-        e->prepared = map_finish(e->ch, &items[k]) == CIO_OK ? 2 : CIO_CORRUPTED;
+    }
+    if (verify_failed) {
+        ctx->last_chunk_error = CIO_ERROR;
     }
     for (size_t i = 0; i < n; i++) {
         struct scan_ent *e = &ents[i];
@@ -1455,7 +1482,7 @@ static void dump_flush(cioa_ctx *ctx, FILE *out, cioa_chunk **ch, int *set_down,
             lens[k] = 2 + (size_t) cioa_st_meta_len(c->map) + (clen > 0 ? (size_t) clen : 0);
             seeds[k] = c->crc_cur;
         }
-        have = cio_crc32_batch_host_multi(bufs, lens, seeds, raw, m, ctx->devs, ctx->ndev) == CIO_OK;
+        have = cioa_crc_batch_route(bufs, lens, seeds, raw, m, ctx->devs, ctx->ndev) == CIO_OK;
     }
     for (size_t k = 0; k < m; k++) {
         cioa_chunk *c = ch[k];

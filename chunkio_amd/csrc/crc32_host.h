@@ -28,6 +28,14 @@ void cioa_stage_fence(void);
 /* Record an error message for cio_gpu_last_error(); returns CIO_ERROR (-1). */
 int cioa_fail_msg(const char *what, const char *detail);
 
+/* crc_route.c: the chunk layer's CRCs over host memory / file ranges -- the
+ * host crc_update when the batch totals at most cio_crc32_cpu_max() bytes,
+ * else the GPU batch (cio_crc32_batch_host_multi / _fd_multi). */
+int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
+                         size_t n, const int *devices, int ndev);
+int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens, const uint32_t *seeds,
+                      uint32_t *out_raw, size_t n, const int *devices, int ndev);
+
 uint32_t cio_crc32_shift(uint32_t raw_state, uint64_t nbytes);
 uint32_t cio_crc32_combine(uint32_t raw_a, uint32_t raw0_b, uint64_t len_b);
 

@@ -326,6 +326,20 @@ void pipe_release(int dev, HostPipe *hp)
     dp.cv.notify_one();
 }
 
+// Releases whatever a slot holds (safe on a partly built slot).
+void slot_free(PipeSlot &s)
+{
+    if (s.done) (void) hipEventDestroy(s.done);
+    if (s.stream) (void) hipStreamDestroy(s.stream);
+    if (s.dbuf) (void) hipFree(s.dbuf);
+    if (s.pinned) (void) hipHostFree(s.pinned);
+    if (s.meta_h) (void) hipHostFree(s.meta_h);
+    if (s.meta_d) (void) hipFree(s.meta_d);
+    if (s.partials) (void) hipFree(s.partials);
+    if (s.counters) (void) hipFree(s.counters);
+    s = PipeSlot();
+}
+
 hipError_t pipe_init(HostPipe &hp)
 {
     hipError_t e = hipSuccess;
@@ -336,10 +350,17 @@ hipError_t pipe_init(HostPipe &hp)
         if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess) break;
         e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     }
-    if (e == hipSuccess) {
-        hp.pool = new CopyPool();
+    if (e != hipSuccess) {
+        // A partial set-up is undone, so the next call's pipe_init starts
+        // from empty slots instead of overwriting (leaking) these.
+        for (int b = 0; b < kSlots; b++) {
+            slot_free(hp.slot[b]);
+        }
+        hp.ready = false;
+        return e;
     }
-    hp.ready = e == hipSuccess;
+    hp.pool = new CopyPool();
+    hp.ready = true;
     return e;
 }
 
@@ -486,6 +507,15 @@ hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
     return hipSuccess;
 }
 
+// The host legs of the last host batch (any thread, any device), for
+// cio_gpu_pipe_last_timing().
+struct PipeTiming {
+    double total_ms = 0, copy_ms = 0, slot_wait_ms = 0, plan_ms = 0, groups = 0, bytes = 0;
+};
+std::mutex g_timing_mu;
+PipeTiming g_last_timing;
+thread_local PipeTiming t_last_timing;
+
 double wall_s()
 {
     struct timespec t;
@@ -566,10 +596,12 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     std::shared_lock<std::shared_mutex> rlk(g_reg_mu);
     int rc = CIO_OK;
     hipEvent_t prev = nullptr;
-    // CIO_GPU_PIPE_TIMING=1: per-call breakdown on stderr (diagnostic)
-    static const bool timing = getenv("CIO_GPU_PIPE_TIMING") != nullptr;
+    // Per-call breakdown, kept for cio_gpu_pipe_last_timing() (a few clock
+    // reads per group); CIO_GPU_PIPE_TIMING=1 also prints it on stderr.
+    static const bool print_timing = getenv("CIO_GPU_PIPE_TIMING") != nullptr;
+    constexpr bool timing = true;
     double t_copy = 0, t_wait = 0, t_plan = 0;
-    const double t_start = timing ? wall_s() : 0;
+    const double t_start = wall_s();
     for (size_t gi = 0; gi < groups.size() && e == hipSuccess && rc == CIO_OK; gi++) {
         PipeSlot &s = hp->slot[gi % kSlots];
         const HostGroup &g = groups[gi];
@@ -641,14 +673,25 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     if (e == hipSuccess && rc == CIO_OK) {
         e = hipMemcpy(out_raw, hp->state, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
     }
-    if (timing) {
+    {
         uint64_t total = 0;
         for (const auto &g : groups) {
             total += g.bytes;
         }
-        fprintf(stderr, "batch_host: dev %d, %zu chunks, %zu groups, %.1f MB: total %.2f ms, copy %.2f ms, "
-                        "slot waits %.2f ms, plans %.2f ms\n", dev, n, groups.size(), total / 1e6,
-                (wall_s() - t_start) * 1e3, t_copy * 1e3, t_wait * 1e3, t_plan * 1e3);
+        PipeTiming &pt = t_last_timing;
+        pt.total_ms = (wall_s() - t_start) * 1e3;
+        pt.copy_ms = t_copy * 1e3;
+        pt.slot_wait_ms = t_wait * 1e3;
+        pt.plan_ms = t_plan * 1e3;
+        pt.groups = (double) groups.size();
+        pt.bytes = (double) total;
+        if (print_timing) {
+            fprintf(stderr, "batch_host: dev %d, %zu chunks, %zu groups, %.1f MB: total %.2f ms, copy %.2f ms, "
+                            "slot waits %.2f ms, plans %.2f ms\n", dev, n, groups.size(), total / 1e6,
+                    pt.total_ms, pt.copy_ms, pt.slot_wait_ms, pt.plan_ms);
+        }
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        g_last_timing = pt;
     }
     if (e != hipSuccess) {
         return fail("cio_crc32_batch_host", e);
@@ -840,6 +883,23 @@ extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t 
     }
     return batch_multi(bufs, nullptr, nullptr, lens, seeds, out_raw, n, devices, ndev,
                        "cio_crc32_batch_host_multi");
+}
+
+extern "C" int cio_gpu_pipe_last_timing(double *out, int n)
+{
+    if (!out || n <= 0) {
+        return fail("cio_gpu_pipe_last_timing: null argument");
+    }
+    PipeTiming pt;
+    {
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        pt = g_last_timing;
+    }
+    const double v[6] = {pt.total_ms, pt.copy_ms, pt.slot_wait_ms, pt.plan_ms, pt.groups, pt.bytes};
+    for (int i = 0; i < n && i < 6; i++) {
+        out[i] = v[i];
+    }
+    return CIO_OK;
 }
 
 extern "C" int cio_gpu_device_count(void)

@@ -14,11 +14,14 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 #include <string>
 #include <vector>
 
 #include "crc32_host.h"
 #include "chunkio_amd/cio_crc32_gpu.h"
+
+static_assert(sizeof(cio_sha1_state) == 96, "cio_sha1_state is the 96-byte C ABI layout");
 
 namespace {
 
@@ -110,6 +113,23 @@ __device__ __forceinline__ void message_block(const uint8_t *p, uint64_t len, ui
     }
 }
 
+// Continuation (cio_sha1_update_batch_dev): block j of the virtual message
+// pending(num bytes, the state's partial block) || data, as 16 big-endian
+// words, byte by byte.  Only block 0 can take pending bytes (num < 64).
+__device__ __forceinline__ void cont_block(const uint8_t *p, const uint8_t *pend, uint32_t num, uint64_t j,
+                                           uint32_t w[16])
+{
+    for (int t = 0; t < 16; ++t) {
+        uint32_t word = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t pos = j * 64 + 4 * t + k;
+            const uint32_t byte = pos < num ? pend[pos] : p[pos - num];
+            word = (word << 8) | byte;
+        }
+        w[t] = word;
+    }
+}
+
 // The 80 rounds of one block from its K_t + W_t rows, folded into the chaining
 // value: 5 VALU per round (two rotates, v_bitop3 round function, add, add3).
 __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20])
@@ -165,9 +185,16 @@ constexpr int kShaThreads = 64 * (1 + kShaSched);
 static_assert(kShaPer % kShaSched == 0, "every schedule wave builds the same number of blocks per group");
 static_assert((kShaAhead * kShaSched) % kShaPer == 0, "a ring turn covers whole groups");
 
+// kCont = false: one-shot digests (SHA1_Init + SHA1_Update + SHA1_Final per
+// chunk).  kCont = true: SHA1_Update over a per-chunk cio_sha1_state: the
+// virtual message is the state's pending bytes || the chunk's bytes; its
+// whole blocks are hashed into the state's chaining value and the rest
+// becomes the new pending block (no padding: sha1_final_kernel pads).
+template <bool kCont>
 __global__ void __launch_bounds__(kShaThreads)
 sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-            const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests, uint32_t n)
+            const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests,
+            cio_sha1_state *__restrict__ states, uint32_t n)
 {
     __shared__ uint4 kw[kShaSlots][kShaRowsPerBlock][64];   // [slot][t / 4][lane] = K + W for t..t+3
     const uint32_t lane = threadIdx.x & 63u;
@@ -178,8 +205,12 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint32_t ic = live ? i : n - 1;
     const uint8_t *p = base + offs[ic];
     const uint64_t len = lens[ic];
-    const uint64_t full = len / 64;
-    const uint64_t nblk = live ? full + ((len - full * 64) < 56 ? 1 : 2) : 0;
+    // pending bytes of the state (kCont); the virtual message starts num bytes before p
+    const uint32_t num = kCont ? (states[ic].num & 63u) : 0u;
+    const uint8_t *pend = kCont ? states[ic].block : nullptr;
+    const uint64_t vlen = len + num;
+    const uint64_t full = vlen / 64;
+    const uint64_t nblk = live ? (kCont ? full : full + ((len - full * 64) < 56 ? 1 : 2)) : 0;
     // The wave's block count: lanes with fewer blocks idle (masked) at the end.
     uint64_t wmax = nblk;
 #pragma unroll
@@ -193,8 +224,14 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         // (this wave's block j + kShaAhead kShaSched is requested when block j
         // is consumed): the 64 lanes read 64 chunks far apart, and one block
         // of prefetch did not cover the HBM latency.
-        const bool aligned = ((uintptr_t) p & 15u) == 0;
-        const uint4 *q = reinterpret_cast<const uint4 *>(p);
+        // Block j's bytes start at vbase + 64 j (vbase = p for one-shot
+        // digests; p - num for a continuation, whose block 0 mixes the
+        // pending bytes with the first data bytes and is gathered bytewise:
+        // lo = 1 keeps every ring load inside the chunk).
+        const uint8_t *vbase = p - num;
+        const bool aligned = ((uintptr_t) vbase & 15u) == 0;
+        const uint4 *q = reinterpret_cast<const uint4 *>(vbase);
+        const uint64_t lo = num > 0 ? 1 : 0;
         constexpr uint64_t kStride = (uint64_t) kShaAhead * kShaSched;
         uint4 nx[kShaAhead][4];
 #pragma unroll
@@ -203,7 +240,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint64_t b = ub < full ? ub : (full ? full - 1 : 0);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                nx[u][v] = (aligned && full > 0) ? q[b * 4 + v] : make_uint4(0, 0, 0, 0);
+                nx[u][v] = (aligned && full > 0 && (!kCont || b >= lo)) ? q[b * 4 + v] : make_uint4(0, 0, 0, 0);
             }
         }
         auto produce = [&](uint64_t j, uint4 (&r)[4]) {
@@ -211,7 +248,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 return;
             }
             uint32_t w[16];
-            if (aligned && j < full) {
+            if (aligned && j < full && (!kCont || j >= lo)) {
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     w[4 * v + 0] = bswap32(r[v].x); w[4 * v + 1] = bswap32(r[v].y);
@@ -223,6 +260,16 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                     r[v] = q[pf * 4 + v];
                 }
                 __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the schedule
+            } else if (kCont) {
+                if (aligned && j + kStride < full) {
+                    // keep the ring slot's next block coming (block 0 took this path)
+                    const uint64_t pf = j + kStride;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        r[v] = q[pf * 4 + v];
+                    }
+                }
+                cont_block(p, pend, num, j, w);
             } else {
                 message_block(p, len, full, j, w);
             }
@@ -264,6 +311,10 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     }
 
     Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    if (kCont && live) {
+        const cio_sha1_state &s0 = states[i];
+        st = {s0.h[0], s0.h[1], s0.h[2], s0.h[3], s0.h[4]};
+    }
     auto load_group = [&](uint64_t g, uint4 (&rows)[kShaPer][kShaRowsPerBlock]) {
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
@@ -304,9 +355,97 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     if (!live) {
         return;
     }
+    if (kCont) {
+        // SHA1_Update's state: chaining value, byte count, and the tail of
+        // the virtual message as the new pending block.  The schedule waves
+        // read the old pending bytes only for block 0, before the first
+        // barrier; with no whole block there is no barrier and this wave
+        // reads them itself (tail byte k is old byte k then).
+        cio_sha1_state &s1 = states[i];
+        const uint32_t rem = (uint32_t) (vlen & 63u);
+        for (uint32_t k = 0; k < rem; ++k) {
+            const uint64_t pos = full * 64 + k;
+            s1.block[k] = pos < num ? pend[pos] : p[pos - num];
+        }
+        s1.h[0] = st.h0; s1.h[1] = st.h1; s1.h[2] = st.h2; s1.h[3] = st.h3; s1.h[4] = st.h4;
+        s1.num = rem;
+        s1.total += len;
+        return;
+    }
     uint8_t *out = digests + (uint64_t) i * 20;
     const uint32_t h[5] = {st.h0, st.h1, st.h2, st.h3, st.h4};
 #pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        out[4 * k + 0] = (uint8_t) (h[k] >> 24);
+        out[4 * k + 1] = (uint8_t) (h[k] >> 16);
+        out[4 * k + 2] = (uint8_t) (h[k] >> 8);
+        out[4 * k + 3] = (uint8_t) h[k];
+    }
+}
+
+// One compression of a block given as 16 big-endian words (schedule inline).
+__device__ void sha1_compress_words(Sha1State &st, uint32_t w[16])
+{
+    uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
+    for (int t = 0; t < 80; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        const uint32_t f = t < 20 ? ch3(b, c, d) : (t < 40 || t >= 60) ? xor3(b, c, d) : maj3(b, c, d);
+        const uint32_t tmp = rotl(a, 5) + f + e + wt + sha1_k(t);
+        e = d;
+        d = c;
+        c = rotl(b, 30);
+        b = a;
+        a = tmp;
+    }
+    st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+}
+
+// SHA1_Final over each state (cio_sha1_final_batch_dev): pad the pending
+// bytes (0x80, zeros, the 64-bit bit count) into 1 or 2 blocks and write the
+// big-endian digest.  The state is left as it was (the pre-Final context
+// cio_sha1_hash exports, src/cio_sha1.c:41-57), so hashing can go on.
+__global__ void sha1_final_kernel(const cio_sha1_state *__restrict__ states, uint8_t *__restrict__ digests,
+                                  uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) {
+        return;
+    }
+    const cio_sha1_state &s0 = states[i];
+    Sha1State st = {s0.h[0], s0.h[1], s0.h[2], s0.h[3], s0.h[4]};
+    const uint32_t num = s0.num & 63u;
+    const uint64_t bits = s0.total * 8;
+    uint32_t w[16];
+    for (int t = 0; t < 16; ++t) {
+        uint32_t word = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pos = 4 * t + k;
+            const uint32_t byte = pos < num ? s0.block[pos] : pos == num ? 0x80u : 0u;
+            word = (word << 8) | byte;
+        }
+        w[t] = word;
+    }
+    if (num < 56) {
+        w[14] = (uint32_t) (bits >> 32);
+        w[15] = (uint32_t) bits;
+        sha1_compress_words(st, w);
+    } else {
+        sha1_compress_words(st, w);
+        for (int t = 0; t < 14; ++t) {
+            w[t] = 0;
+        }
+        w[14] = (uint32_t) (bits >> 32);
+        w[15] = (uint32_t) bits;
+        sha1_compress_words(st, w);
+    }
+    uint8_t *out = digests + (uint64_t) i * 20;
+    const uint32_t h[5] = {st.h0, st.h1, st.h2, st.h3, st.h4};
     for (int k = 0; k < 5; ++k) {
         out[4 * k + 0] = (uint8_t) (h[k] >> 24);
         out[4 * k + 1] = (uint8_t) (h[k] >> 16);
@@ -320,18 +459,74 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
 namespace {
 
 int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens, uint8_t *dev_digests,
-                size_t n, hipStream_t s)
+                cio_sha1_state *dev_states, size_t n, hipStream_t s)
 {
     if (n > 0xFFFFFFFFull - 63) {
         return cioa_fail_msg("cio_sha1_batch_dev", "too many chunks for one launch");
     }
-    hipLaunchKernelGGL(sha1_kernel, dim3((uint32_t) ((n + 63) / 64)), dim3(kShaThreads), 0, s,
-                       reinterpret_cast<const uint8_t *>(dev_base), dev_offs, dev_lens, dev_digests, (uint32_t) n);
+    const dim3 grid((uint32_t) ((n + 63) / 64));
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(dev_base);
+    if (dev_states) {
+        hipLaunchKernelGGL(sha1_kernel<true>, grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens, nullptr,
+                           dev_states, (uint32_t) n);
+    } else {
+        hipLaunchKernelGGL(sha1_kernel<false>, grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens, dev_digests,
+                           nullptr, (uint32_t) n);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev: launch", hipGetErrorString(e));
 }
 
 }  // namespace
+
+extern "C" void cio_sha1_state_init(cio_sha1_state *states, size_t n)
+{
+    for (size_t k = 0; k < n; k++) {
+        cio_sha1_state &s0 = states[k];
+        memset(&s0, 0, sizeof(s0));
+        s0.h[0] = 0x67452301u;
+        s0.h[1] = 0xEFCDAB89u;
+        s0.h[2] = 0x98BADCFEu;
+        s0.h[3] = 0x10325476u;
+        s0.h[4] = 0xC3D2E1F0u;
+    }
+}
+
+extern "C" int cio_sha1_update_batch_dev(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens,
+                                         cio_sha1_state *dev_states, size_t n, void *stream)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (dev_base == nullptr || dev_offs == nullptr || dev_lens == nullptr || dev_states == nullptr) {
+        return cioa_fail_msg("cio_sha1_update_batch_dev", "null pointer");
+    }
+    if (cio_gpu_init() != CIO_OK) {
+        return CIO_ERROR;
+    }
+    return sha1_launch(dev_base, dev_offs, dev_lens, nullptr, dev_states, n, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int cio_sha1_final_batch_dev(const cio_sha1_state *dev_states, uint8_t *dev_digests, size_t n,
+                                        void *stream)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    if (dev_states == nullptr || dev_digests == nullptr) {
+        return cioa_fail_msg("cio_sha1_final_batch_dev", "null pointer");
+    }
+    if (n > 0xFFFFFFFFull - 255) {
+        return cioa_fail_msg("cio_sha1_final_batch_dev", "too many chunks for one launch");
+    }
+    if (cio_gpu_init() != CIO_OK) {
+        return CIO_ERROR;
+    }
+    hipLaunchKernelGGL(sha1_final_kernel, dim3((uint32_t) ((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), dev_states, dev_digests, (uint32_t) n);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_final_batch_dev: launch", hipGetErrorString(e));
+}
 
 extern "C" int cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens,
                                         uint8_t *dev_digests, size_t n, void *stream)
@@ -345,7 +540,7 @@ extern "C" int cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *de
     if (cio_gpu_init() != CIO_OK) {
         return CIO_ERROR;
     }
-    return sha1_launch(dev_base, dev_offs, dev_lens, dev_digests, n, reinterpret_cast<hipStream_t>(stream));
+    return sha1_launch(dev_base, dev_offs, dev_lens, dev_digests, nullptr, n, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, const uint64_t *lens,
@@ -374,7 +569,7 @@ extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, co
         (void) hipFree(d);
         return cioa_fail_msg("cio_sha1_batch_dev: copy", hipGetErrorString(e));
     }
-    const int rc = sha1_launch(dev_base, d, d + n, dev_digests, n, s);
+    const int rc = sha1_launch(dev_base, d, d + n, dev_digests, nullptr, n, s);
     e = hipStreamSynchronize(s);
     (void) hipFree(d);
     if (rc != CIO_OK) {

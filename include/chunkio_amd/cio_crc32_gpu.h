@@ -28,6 +28,10 @@
  *                                    (src/cio_file.c:97-113)
  *   cio_sha1_batch_dev()             cio_sha1_init/update/final over each chunk
  *                                    (src/cio_sha1.c:26-57)
+ *   cio_sha1_update/final_batch_dev  cio_sha1_update / cio_sha1_final on a
+ *                                    carried context per chunk (src/cio_sha1.c:
+ *                                    31-39), incl. the pre-Final state export of
+ *                                    cio_sha1_hash (:41-57)
  *
  * CRC values in and out are RAW states (not finalized), exactly what
  * crc_update() takes and returns: seed 0xffffffff (= crc_init()) gives the
@@ -162,6 +166,26 @@ int  cio_crc32_batch_fd_multi(const int *fds, const uint64_t *foffs, const size_
 int  cio_crc32_host_register(const void *p, size_t len);
 int  cio_crc32_host_unregister(const void *p);
 
+/* Host-side legs of the last host/file batch that finished (any thread; per
+ * device entry for *_multi): out[0..5] = total ms, copy into pinned staging
+ * ms (caller thread's share of the pool's wall time), slot waits ms, plan
+ * builds ms, staging groups, staged bytes.  Fills min(n, 6) values. */
+int  cio_gpu_pipe_last_timing(double *out, int n);
+
+/* Small-batch routing of the chunk layer.  The verify/sync batches
+ * (cio_verify.h, cio_sync.h) and the chunk API (cioa_chunk.h) compute a
+ * batch whose regions total at most cio_crc32_cpu_max() bytes with the
+ * library's crc_update on the calling thread instead of a GPU round trip
+ * (one chunk's verify on open/up, a recompute after write_at, a deferred
+ * catch-up); larger batches take the GPU path above.  Same results either
+ * way.  The default is the measured crossover of one-chunk GPU host batches
+ * against crc_update (profiles/r03/crossover_*.txt); the environment
+ * variable CIOA_CPU_CRC_MAX (bytes) or cio_crc32_set_cpu_max() overrides it,
+ * 0 sends everything to the GPU.  The cio_crc32_batch_* entry points above
+ * never route: they always run on the GPU. */
+size_t cio_crc32_cpu_max(void);
+void   cio_crc32_set_cpu_max(size_t bytes);
+
 /* ---- synthetic data (benchmarks / tests) ------------------------------- */
 
 /* Fill dev_base + offs[i] .. + lens[i] with the deterministic generator
@@ -186,6 +210,41 @@ int  cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs,
  * cio_crc32_plan_exec. */
 int  cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *dev_offs,
                               const uint64_t *dev_lens, uint8_t *dev_digests,
+                              size_t n, void *stream);
+
+/* ---- SHA-1 with continuation (SHA1_Init / SHA1_Update / SHA1_Final) ----- */
+
+/* Per-chunk SHA-1 context, the state cio_sha1_init/update/final carry in an
+ * SHA_CTX (src/cio_sha1.c:26-39) and cio_sha1_hash can export before its
+ * SHA1_Final "for future iterations and updates" (:41-57): chaining value,
+ * bytes hashed so far, and the pending partial block.  96 bytes, plain data:
+ * arrays of it live in device memory for the batch calls below. */
+typedef struct cio_sha1_state {
+    uint32_t h[5];        /* chaining value H0..H4 */
+    uint32_t num;         /* bytes pending in block[] (0..63) */
+    uint64_t total;       /* message bytes hashed so far, pending ones included */
+    uint8_t  block[64];   /* pending partial block */
+} cio_sha1_state;
+
+/* SHA1_Init of n states in HOST memory (copy them to the device after). */
+void cio_sha1_state_init(cio_sha1_state *states, size_t n);
+
+/* SHA1_Update of chunk i (dev_base + dev_offs[i], dev_lens[i] bytes) into
+ * dev_states[i], for every i in one launch (device arrays, no allocation, no
+ * host synchronisation).  Any split is allowed: a chunk may continue from a
+ * state whose pending block is partial, and zero-length updates are no-ops.
+ * When the continued byte stream is 16-byte aligned in memory (data at
+ * p with (p - num) 16-byte aligned: e.g. a chunk's mapped content appended
+ * in place), every block after the first is read by the fast vector path;
+ * otherwise blocks are gathered bytewise (correct, slower). */
+int  cio_sha1_update_batch_dev(const void *dev_base, const uint64_t *dev_offs,
+                               const uint64_t *dev_lens, cio_sha1_state *dev_states,
+                               size_t n, void *stream);
+
+/* SHA1_Final of every state into dev_digests + 20 i (big-endian).  The
+ * states are NOT modified, so each stays the pre-Final context and can be
+ * updated further (cio_sha1_hash's export, src/cio_sha1.c:41-57). */
+int  cio_sha1_final_batch_dev(const cio_sha1_state *dev_states, uint8_t *dev_digests,
                               size_t n, void *stream);
 
 /* ---- diagnostics -------------------------------------------------------- */

@@ -87,7 +87,10 @@ int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags,
  * pipeline (cio_crc32_batch_fd_multi: pread through a per-thread bounce
  * buffer, streaming stores into pinned staging).  With CIOA_VERIFY_WRITEBACK the files
  * are opened read-write (inferred legacy lengths written back, empty files
- * initialised).  With CIOA_VERIFY_DELETE_IRRECOVERABLE the irrecoverable
+ * initialised and, since this call also closes them, left as the reference's
+ * close leaves them: synced, with htonl(crc_finalize(0xBE26ED00)) =
+ * 41 d9 12 ff in the CRC field when checksums are on, so the next verify
+ * passes).  With CIOA_VERIFY_DELETE_IRRECOVERABLE the irrecoverable
  * files are unlinked after the batch, as cio_scan does. */
 int cio_verify_paths(const char *const *paths, size_t n, int flags, int *status,
                      int *error, uint32_t *crc_raw);

@@ -122,11 +122,17 @@ size_t cioa_stream_chunks(cioa_stream *st, cioa_chunk **out, size_t cap);
 
 /* Verify-on-load of root_path/<stream> (cio_scan_stream_files): every
  * regular file not starting with '.' (and ending in chunk_extension if
- * given) becomes a chunk.  Up to the max_chunks_up budget they are opened,
- * mapped and verified in ONE batched GPU pass; the rest are registered down
- * (unverified, as the reference leaves them).  A chunk that fails its load
- * is not registered; with CIO_DELETE_IRRECOVERABLE the file is deleted when
- * the failure was BAD_CHECKSUM / BAD_FILE_SIZE / BAD_LAYOUT.  Returns the
+ * given) becomes a chunk, in name order.  Up to the free max_chunks_up
+ * slots they are opened, mapped and verified in ONE batched GPU pass; as in
+ * the reference a chunk takes a slot only once it passed (cio_file.c:490),
+ * so when some fail, the freed slots go to the next files in another batch.
+ * The rest are registered down (unverified, as the reference leaves them).
+ * A chunk that fails its load is not registered; with
+ * CIO_DELETE_IRRECOVERABLE the file is deleted when the failure was
+ * BAD_CHECKSUM / BAD_FILE_SIZE / BAD_LAYOUT.  If a batch cannot run at all
+ * (GPU failure), its chunks are registered down, unverified (a later
+ * cioa_chunk_up verifies them), and cioa_last_chunk_error() returns
+ * CIO_ERROR afterwards (cio_gpu_last_error() has the reason).  Returns the
  * stream (created if needed) or NULL. */
 cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *chunk_extension);
 

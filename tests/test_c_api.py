@@ -9,7 +9,9 @@ test_chunk_api: the reference's tests/fs.c and tests/metadata_update.c
 replayed through include/chunkio_amd/cioa_chunk.h, plus transactions, trim,
 full sync, batched scan with CIO_DELETE_IRRECOVERABLE and deferred/immediate
 byte identity; in the reference's per-write order (immediate) and with the
-CRC deferred to batched GPU syncs (deferred).  Verifies run on the GPU.
+CRC deferred to batched GPU syncs (deferred).  Verifies run on the GPU
+(CIOA_CPU_CRC_MAX=0) under -m gpu, and on the host CRC route in the CPU
+suite.
 """
 import os
 import subprocess
@@ -28,8 +30,9 @@ def _bin(name):
     return p
 
 
-def _run(args, timeout=600):
-    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+def _run(args, timeout=600, env=None):
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout,
+                       env=None if env is None else {**os.environ, **env})
     return r.returncode, r.stdout + r.stderr
 
 
@@ -55,9 +58,19 @@ def test_chunk_api_cpu_paths(tmp_path, name):
 
 @pytest.mark.gpu
 def test_chunk_api_reference_tests_immediate_and_deferred(cuda, tmp_path):
-    rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), "immediate"])
-    print(out)
-    assert rc == 0, out
-    rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), "deferred"])
-    print(out)
-    assert rc == 0, out
+    """Every verify, recompute and deferred sync on the GPU route
+    (CIOA_CPU_CRC_MAX=0: no batch is small enough for the host CRC)."""
+    for mode in ("immediate", "deferred"):
+        rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), mode], env={"CIOA_CPU_CRC_MAX": "0"})
+        print(out)
+        assert rc == 0, out
+
+
+def test_chunk_api_reference_tests_host_route(tmp_path):
+    """The same C replay with every chunk-layer CRC on the library's host
+    crc_update (CIOA_CPU_CRC_MAX huge, crc_route.c): the chunk API's
+    semantics do not depend on where the CRC runs.  (The deferred run
+    compares its identity corpus with the immediate run's files.)"""
+    for mode in ("immediate", "deferred"):
+        rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), mode], env={"CIOA_CPU_CRC_MAX": str(1 << 62)})
+        assert rc == 0 and "0 failed" in out, out

@@ -16,6 +16,27 @@ from oracle import pyoracle as po
 
 INIT = 0xFFFFFFFF
 
+# Where the chunk layer's CRCs run (crc_route.c): "host" sends every batch to
+# the library's crc_update, "gpu" sends every batch to the GPU pipeline
+# (cio_crc32_set_cpu_max(0)); the default in between is the measured
+# crossover.  Each chunk-layer test runs both ways: the host route in the CPU
+# suite, the GPU route under -m gpu.  Results must not depend on the route.
+ROUTES = [pytest.param("host", id="host"), pytest.param("gpu", marks=pytest.mark.gpu, id="gpu")]
+
+
+@pytest.fixture
+def route(request):
+    from chunkio_amd import _lib
+    lib = _lib.lib()
+    old = lib.cio_crc32_cpu_max()
+    if request.param == "gpu":
+        request.getfixturevalue("cuda")
+        lib.cio_crc32_set_cpu_max(0)
+    else:
+        lib.cio_crc32_set_cpu_max(1 << 62)
+    yield request.param
+    lib.cio_crc32_set_cpu_max(old)
+
 
 def hdr_crc_be(path):
     with open(path, "rb") as f:
@@ -125,8 +146,8 @@ def test_verify_delete_irrecoverable_without_crc(tmp_path):
 
 # ---------------------------------------------------------------- GPU verify
 
-@pytest.mark.gpu
-def test_down_up_keeps_crc(cuda, tmp_path, data400):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_down_up_keeps_crc(route, tmp_path, data400):
     # tests/fs.c:293-432: CRC survives down/up; up re-verifies the whole region
     p = str(tmp_path / "updown")
     c, _ = cf.ChunkFile.open(p)
@@ -147,8 +168,8 @@ def test_down_up_keeps_crc(cuda, tmp_path, data400):
     c2.close()
 
 
-@pytest.mark.gpu
-def test_issue_write_at_and_corruption(cuda, tmp_path):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_issue_write_at_and_corruption(route, tmp_path):
     # tests/fs.c:633-724
     p = str(tmp_path / "test")
     c, _ = cf.ChunkFile.open(p)
@@ -167,9 +188,9 @@ def test_issue_write_at_and_corruption(cuda, tmp_path):
     assert c.map is None and not c.is_up()                      # map released, fd closed
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
 @pytest.mark.parametrize("trigger_error", [False, True])
-def test_legacy_content_length(cuda, tmp_path, data400, trigger_error):
+def test_legacy_content_length(route, tmp_path, data400, trigger_error):
     # tests/fs.c:851-965: zeroed length field, file truncated to 128+24 (ok) / 128+25 (bad)
     p = str(tmp_path / "test_chunk")
     c, _ = cf.ChunkFile.open(p)
@@ -190,8 +211,8 @@ def test_legacy_content_length(cuda, tmp_path, data400, trigger_error):
         c.close()
 
 
-@pytest.mark.gpu
-def test_metadata_update_recompute(cuda, tmp_path, data400):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_metadata_update_recompute(route, tmp_path, data400):
     # tests/metadata_update.c: metadata moves content, CRC recomputed, verify on reload
     p = str(tmp_path / "meta")
     c, _ = cf.ChunkFile.open(p)
@@ -209,8 +230,8 @@ def test_metadata_update_recompute(cuda, tmp_path, data400):
     c2.close()
 
 
-@pytest.mark.gpu
-def test_batched_scan_verify(cuda, tmp_path):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_batched_scan_verify(route, tmp_path):
     rng = np.random.default_rng(31)
     paths, expect = [], []
     for i in range(300):
@@ -276,8 +297,8 @@ def _apply(c, ops):
             c.write_metadata(data)
 
 
-@pytest.mark.gpu
-def test_deferred_crc_batch_sync_matches_reference_sequence(cuda, tmp_path):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_deferred_crc_batch_sync_matches_reference_sequence(route, tmp_path):
     # f3: appends without the CRC, then ONE GPU batch sync (cio_file_sync_batch)
     # must leave every file byte-identical to the reference's write/sync path.
     rng = np.random.default_rng(41)
@@ -313,8 +334,8 @@ def test_deferred_crc_batch_sync_matches_reference_sequence(cuda, tmp_path):
     assert len(ok) >= 100
 
 
-@pytest.mark.gpu
-def test_deferred_crc_perf_files_and_reopen_append(cuda, tmp_path, data400):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_deferred_crc_perf_files_and_reopen_append(route, tmp_path, data400):
     # the `cio -k -p` file shape, synced as one batch: every header is c1 00 08 87 40 e7 00..
     files = []
     for i in range(16):
@@ -338,8 +359,8 @@ def test_deferred_crc_perf_files_and_reopen_append(cuda, tmp_path, data400):
     assert cf.verify_paths([str(tmp_path / "perf-test-0003.txt")])[0][0] == cf.CIO_OK
 
 
-@pytest.mark.gpu
-def test_sync_batch_rejects_bad_items(cuda, tmp_path):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_sync_batch_rejects_bad_items(route, tmp_path):
     import ctypes
     import mmap
     # a chunk image with 5000 content bytes and a fresh (unsynced) CRC state
@@ -375,8 +396,8 @@ def test_sync_batch_rejects_bad_items(cuda, tmp_path):
     os.close(fd)
 
 
-@pytest.mark.gpu
-def test_tx_rollback_deferred_matches_immediate(cuda, tmp_path, data400):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_tx_rollback_deferred_matches_immediate(route, tmp_path, data400):
     """cio_chunk_tx_begin/commit/rollback (src/cio_chunk.c:423-502): crc_cur
     restored as a uint32 with data_size; deferred and immediate chunks driven
     the same way end byte-identical."""
@@ -406,8 +427,8 @@ def test_tx_rollback_deferred_matches_immediate(cuda, tmp_path, data400):
     assert out["imm"][1] == want
 
 
-@pytest.mark.gpu
-def test_scan_stream_delete_irrecoverable(cuda, tmp_path):
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_scan_stream_delete_irrecoverable(route, tmp_path):
     ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM, max_chunks_up=100)
     st = ctx.stream("s")
     for i in range(20):
@@ -449,9 +470,9 @@ def _expected_dump(root, streams, checksum):
     return "".join(out)
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
 @pytest.mark.parametrize("flags", [cf.CIO_CHECKSUM, 0, cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC])
-def test_scan_dump_listing(cuda, tmp_path, data400, flags):
+def test_scan_dump_listing(route, tmp_path, data400, flags):
     # tools/cio -l: a synced chunk with metadata, an unsynced one, a down one,
     # and a chunk loaded by a stream scan (its crc_cur is the verified CRC, so
     # the reference's dump reports it as a checksum error: SURVEY a15).
@@ -509,3 +530,91 @@ def test_scan_dump_listing(cuda, tmp_path, data400, flags):
         want = _expected_dump(root, views, flags & cf.CIO_CHECKSUM)
         assert text == want, (text, want)
         assert "d.flb" in text and "unsynced" not in text
+
+
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_verify_empty_writeback_twice_keeps_file(route, tmp_path):
+    """an empty file verified read-write with checksums on is
+    prepared AND closed by cio_verify_paths, so it must be left as the
+    reference's close leaves it (mmap_file marks it unsynced, munmap_file
+    syncs, finalize_checksum stores htonl(crc_finalize(crc_cur)):
+    41 d9 12 ff 00 00 00 00) -- and verify again, here and in the reference."""
+    empty = tmp_path / "empty"
+    empty.write_bytes(b"")
+    rw = cf.CIO_CHECKSUM | cf.CIOA_VERIFY_WRITEBACK
+    st, er, crc = cf.verify_paths([str(empty)], flags=rw)
+    assert (int(st[0]), int(er[0]), int(crc[0])) == (cf.CIO_OK, 0, 0xBE26ED00)
+    raw = empty.read_bytes()
+    assert raw[:10] == bytes([0xC1, 0x00, 0x41, 0xD9, 0x12, 0xFF]) + bytes(4)
+    assert struct.unpack(">I", raw[2:6])[0] == po.crc_update(INIT, b"\0\0") ^ INIT   # tests/fs.c:201-206
+    st, er, crc = cf.verify_paths([str(empty)], flags=rw)
+    assert (int(st[0]), int(er[0]), int(crc[0])) == (cf.CIO_OK, 0, 0xBE26ED00)
+    st, er, crc = cf.verify_paths([str(empty)], flags=cf.CIO_CHECKSUM | cf.CIO_DELETE_IRRECOVERABLE)
+    assert (int(st[0]), int(er[0])) == (cf.CIO_OK, 0)
+    assert empty.exists()
+    c, rc = cf.ChunkFile.open(str(empty))                       # the chunk API loads it too
+    assert rc == cf.CIO_OK and c.crc_cur == 0xBE26ED00 and c.data_size == 0
+    c.close()
+
+
+def _make_stream(tmp_path, n, corrupt=()):
+    ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM, max_chunks_up=100)
+    st = ctx.stream("s")
+    for i in range(n):
+        c, _ = st.open(f"c{i:02d}")
+        c.write(bytes([65 + i]) * (700 * i + 3))
+    ctx.close()
+    for i in corrupt:
+        raw = bytearray((tmp_path / "s" / f"c{i:02d}").read_bytes())
+        raw[24] ^= 1                                            # first content byte
+        (tmp_path / "s" / f"c{i:02d}").write_bytes(bytes(raw))
+
+
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_scan_budget_counts_only_loaded_chunks(route, tmp_path):
+    """with max_chunks_up = 3 and c01 corrupted, the reference
+    loads c00, c02, c03 (a chunk takes a slot only after its format check,
+    src/cio_file.c:490) and registers c04, c05 down, unverified (:566)."""
+    _make_stream(tmp_path, 6, corrupt=(1,))
+    ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM | cf.CIO_DELETE_IRRECOVERABLE, max_chunks_up=3)
+    st, chunks = ctx.scan("s")
+    assert [(c.name, c.is_up()) for c in chunks] == [("c00", True), ("c02", True), ("c03", True),
+                                                       ("c04", False), ("c05", False)]
+    assert ctx.total_chunks_up == 3
+    assert ctx.last_chunk_error == cf.CIO_ERR_BAD_CHECKSUM
+    assert [c.data_size for c in chunks if c.is_up()] == [3, 1403, 2103]
+    ctx.close()
+    assert not (tmp_path / "s" / "c01").exists()
+    # every slot failing: the next files get the slots
+    _make_stream(tmp_path / "b", 6, corrupt=(0, 1, 2))
+    ctx = cf.Context(str(tmp_path / "b"), cf.CIO_CHECKSUM, max_chunks_up=2)
+    st, chunks = ctx.scan("s")
+    assert [(c.name, c.is_up()) for c in chunks] == [("c03", True), ("c04", True), ("c05", False)]
+    ctx.close()
+
+
+def test_scan_verify_failure_registers_down(tmp_path):
+    """when the batched verify cannot run at all (here: the GPU
+    route forced with cio_crc32_set_cpu_max(0) and a device ordinal that
+    does not exist), the scan keeps every chunk it covered, registered down
+    and unverified, reports CIO_ERROR through cioa_last_chunk_error(), and
+    deletes nothing; up() verifies them once a CRC path works."""
+    from chunkio_amd import _lib
+    lib = _lib.lib()
+    _make_stream(tmp_path, 4, corrupt=(2,))
+    old = lib.cio_crc32_cpu_max()
+    lib.cio_crc32_set_cpu_max(0)
+    try:
+        ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM | cf.CIO_DELETE_IRRECOVERABLE, devices=[99],
+                         max_chunks_up=100)
+        st, chunks = ctx.scan("s")
+        assert [(c.name, c.is_up()) for c in chunks] == [(f"c{i:02d}", False) for i in range(4)]
+        assert ctx.last_chunk_error == cf.CIO_ERROR
+        assert ctx.total_chunks_up == 0
+        assert (tmp_path / "s" / "c02").exists()
+        lib.cio_crc32_set_cpu_max(1 << 62)                      # a working (host) CRC route
+        assert [c.up() for c in chunks] == [cf.CIO_OK, cf.CIO_OK, cf.CIO_CORRUPTED, cf.CIO_OK]
+        assert [c.data_size for c in chunks if c.is_up()] == [3, 703, 2103]
+        ctx.close()
+    finally:
+        lib.cio_crc32_set_cpu_max(old)

@@ -140,6 +140,20 @@ def test_bench_gpus_n_spawns_ranks_or_refuses(tmp_path):
     assert r.stdout == ""
 
 
+def test_bench_spawn_parent_counts_gpus_without_torch():
+    """The spawn parent counts GPUs from sysfs and never imports torch (so it
+    cannot initialise the GPU before its children start); here, no GPU."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import bench; n, how = bench.visible_gpus(); "
+            "print(n, how.split('+')[0], 'torch' in sys.modules)" % root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    n, how, imported = r.stdout.split()
+    assert (n, how, imported) == ("0", "kfd-sysfs", "False")
+
+
 def test_bench_traffic_scales_to_a_shards_launch():
     """roofline.traffic at N > 1: a strong-scaled cfg4 shard launches 1/N of the
     bytes the committed N = 1 PMC pass profiled, so the bench applies that

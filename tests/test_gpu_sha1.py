@@ -100,3 +100,101 @@ def test_many_workgroups_ragged_and_misaligned(cuda):
     for i in range(n):
         o, ln = int(offs[i]), int(lens[i])
         assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
+
+
+# ---- continuation: SHA1_Init / SHA1_Update / SHA1_Final per chunk ---------
+# (cio_sha1_update_batch_dev / cio_sha1_final_batch_dev; the reference's
+# cio_sha1_init/update/final, src/cio_sha1.c:26-39, and the pre-Final state
+# export of cio_sha1_hash, :41-57)
+
+def _dev_i64(a, cuda):
+    import torch
+    return torch.from_numpy(np.asarray(a, dtype=np.int64)).to(cuda)
+
+
+def test_continuation_random_splits(cuda):
+    """Three updates per chunk at random split points (any byte, not only
+    64-byte multiples, empty pieces included), the byte stream contiguous in
+    memory at random 16-byte-aligned and unaligned bases: after every update
+    the final digest equals hashlib over the prefix, and the exported state
+    holds the prefix's byte count and pending tail."""
+    import torch
+    rng = np.random.default_rng(71)
+    n = 300
+    lens = rng.integers(0, 20000, n).astype(np.uint64)
+    lens[:8] = [0, 1, 63, 64, 65, 119, 128, 4096]
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 40, n - 1).astype(np.uint64))
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    dev = torch.from_numpy(host).to(cuda)
+    cuts = np.sort(np.stack([rng.integers(0, lens.astype(np.int64) + 1) for _ in range(2)], axis=1), axis=1)
+    cuts[:40:4, 0] = (cuts[:40:4, 0] // 64) * 64          # some block-aligned splits
+    bounds = np.concatenate([np.zeros((n, 1), np.int64), cuts, lens.astype(np.int64)[:, None]], axis=1)
+    states = cio.sha1_states_init(n, cuda)
+    for stage in range(3):
+        a, b = bounds[:, stage], bounds[:, stage + 1]
+        cio.sha1_update_batch_dev(dev, _dev_i64(offs.astype(np.int64) + a, cuda), _dev_i64(b - a, cuda), states)
+        got = cio.sha1_final_batch_dev(states)
+        view = cio.sha1_states_view(states)
+        for i in range(n):
+            pre = host[int(offs[i]):int(offs[i]) + int(b[i])].tobytes()
+            assert bytes(got[i]) == hashlib.sha1(pre).digest(), (stage, i)
+            assert int(view["total"][i]) == len(pre) and int(view["num"][i]) == len(pre) % 64, (stage, i)
+            k = len(pre) % 64
+            assert view["block"][i, :k].tobytes() == pre[len(pre) - k:], (stage, i)
+    # the full-message digests also equal the one-shot kernel's
+    assert np.array_equal(cio.sha1_final_batch_dev(states), cio.sha1_batch_dev(dev, offs, lens))
+
+
+def test_continuation_across_buffers_and_final_keeps_state(cuda):
+    """A from one buffer, B from another at an unrelated (misaligned) address:
+    the continued context is only the 96-byte state.  Final leaves the state
+    untouched, so hashing continues after a digest was taken."""
+    import torch
+    rng = np.random.default_rng(72)
+    n = 130
+    la = rng.integers(0, 3000, n)
+    lb = rng.integers(0, 3000, n)
+    A = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in la]
+    B = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in lb]
+    from test_gpu_crc import pack, to_dev
+    bufa, oa, _ = pack(A, misalign=[int(x) for x in rng.integers(0, 16, n)])
+    bufb, ob, _ = pack(B, misalign=[int(x) for x in rng.integers(0, 16, n)])
+    da, db = to_dev(bufa, cuda), to_dev(bufb, cuda)
+    states = cio.sha1_states_init(n, cuda)
+    cio.sha1_update_batch_dev(da, _dev_i64(oa, cuda), _dev_i64(la, cuda), states)
+    before = states.clone()
+    got_a = cio.sha1_final_batch_dev(states)
+    assert torch.equal(states, before)
+    assert [bytes(d) for d in got_a] == [hashlib.sha1(x).digest() for x in A]
+    cio.sha1_update_batch_dev(db, _dev_i64(ob, cuda), _dev_i64(lb, cuda), states)
+    cio.sha1_update_batch_dev(db, _dev_i64(ob, cuda), _dev_i64(np.zeros(n), cuda), states)   # empty updates
+    got = cio.sha1_final_batch_dev(states)
+    assert [bytes(d) for d in got] == [hashlib.sha1(x + y).digest() for x, y in zip(A, B)]
+
+
+def test_continuation_appends_cfg5_shape(cuda, golden):
+    """The cfg5 batch hashed as a chunk grows in place: five 81,920-byte
+    appends per 409,600-byte chunk (block-aligned stream, the fast path
+    after block 0), then one 7-byte append per chunk and its digest."""
+    import torch
+    lens = wl.cfg2_lens()
+    offs = wl.packed_offsets(lens, align=16)
+    dev = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, wl.CFG2_SEED)
+    n = len(lens)
+    states = cio.sha1_states_init(n, cuda)
+    step = 81920
+    for k in range(5):
+        cio.sha1_update_batch_dev(dev, _dev_i64(offs.astype(np.int64) + k * step, cuda),
+                                  _dev_i64(np.full(n, step), cuda), states)
+    got = cio.sha1_final_batch_dev(states)
+    assert [bytes(d).hex() for d in got[:8]] == golden["sha1"]["cfg2_first8"]
+    assert np.array_equal(got, cio.sha1_batch_dev(dev, offs, lens))
+    tail = torch.arange(7, dtype=torch.uint8, device=cuda) + 1
+    cio.sha1_update_batch_dev(tail, _dev_i64(np.zeros(n), cuda), _dev_i64(np.full(n, 7), cuda), states)
+    got7 = cio.sha1_final_batch_dev(states)
+    host = dev.cpu().numpy()
+    for i in (0, 511, n - 1):
+        msg = host[int(offs[i]):int(offs[i] + lens[i])].tobytes() + bytes(range(1, 8))
+        assert bytes(got7[i]) == hashlib.sha1(msg).digest(), i
