@@ -111,6 +111,7 @@ struct cio_crc32_plan {
     uint64_t ustride = 0, ua0 = 0, uvlen = 0;   // uniform batch geometry (unsteps > 0)
     uint32_t unsteps = 0, uh = 0;
     bool small = false;        // every chunk fits one wave-step: crc32_small_kernel
+    bool ahead = false;        // uniform, 16-B aligned, whole 4 KiB steps: issue-ahead stream kernel
     unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     cioa::ChunkDesc *desc = nullptr;

@@ -556,7 +556,12 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 #ifndef CIO_LDS_FOLD
 #define CIO_LDS_FOLD 1
 #endif
-template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false>
+// AHEAD (uniform batches of whole 4 KiB steps with no alignment head: every
+// step is full, so the partial-step paths compile out): two ring slots, and
+// the next step's loads are issued as soon as this step's data has landed,
+// BEFORE its CRC -- still one step (4 KiB) in flight per wave, as in the
+// read-only stream, but no longer none while the wave computes.
+template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false, bool AHEAD = false>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
                     uint32_t W, uint32_t unsteps, uint32_t uh, uint32_t n,
@@ -631,9 +636,18 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 
     auto issue = [&](StepRegs &r) {
         // Past the wave's range the last step is re-read (cache-resident) so
-        // that every refill is the same 4 loads.
+        // that every refill is the same 4 loads.  AHEAD refills past the
+        // range (its last one or two) read the 4 KiB slice table instead: a
+        // branch-free select keeps one load sequence on every path, so the
+        // compiler's vmcnt waits stay exact, and the table is L2-resident.
+        if (AHEAD) {
+            const bool real = nload > 0;
+            const uint8_t *src = real ? lbase + ld.a : reinterpret_cast<const uint8_t *>(g_slice);
+            load_step(r, src, real ? lj : 0, real ? ld.vlen : (uint64_t) kStep, lane);
+        } else {
         const uint64_t jj = nload > 0 ? lj : (uint64_t) ld.nsteps - 1;
         load_step(r, lbase + ld.a, jj, ld.vlen, lane);
+        }
         if (nload > 0) {
             --nload;
             if (++lj == ld.nsteps && nload > 0) {
@@ -731,7 +745,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // step's loads are issued, so their latency overlaps the fold.
         auto crc_step = [&](StepRegs &r) -> bool {
             {
-                if (j < full_end) {
+                if (AHEAD || j < full_end) {
                     // The 4080-byte jump of every sub-chain needs only its
                     // state: its lookups go out before the first use of the
                     // step's data, so after the data lands only the four
@@ -748,10 +762,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                     for (int q = 0; q < kSub; ++q) {
                         s[q] = block16(lds, lb_lo, lb_hi, h[q], r.q[q]);
                     }
-                    const uint64_t e0 = j * kStep + (uint64_t) (lane + 1) * kGran;
+                    if (!AHEAD) {
+                        const uint64_t e0 = j * kStep + (uint64_t) (lane + 1) * kGran;
 #pragma unroll
-                    for (int q = 0; q < kSub; ++q) {
-                        e[q] = e0 + (uint64_t) q * kRow;
+                        for (int q = 0; q < kSub; ++q) {
+                            e[q] = e0 + (uint64_t) q * kRow;
+                        }
                     }
                 } else {
                     slow_compute(lds, lb_lo, lb_hi, lrep, r, j, d.vlen, d.h, seed, lane, s, e);
@@ -767,7 +783,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             {
                 {
                     uint32_t contrib;
-                    if (j <= full_end) {
+                    if (AHEAD || j <= full_end) {
                         // The last step was full: Horner over the sub-chains
                         // with the constant x^(8 * 1024), then the lane factor.
                         // (The asm keeps the compiler from hoisting xl's 32
@@ -837,7 +853,46 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // shifted to the chunk end and no fold multiplies.  Computed in the
         // second iteration (the first if there is one), off the start-up path.
         const uint64_t it_f = iters > 1 ? 1 : 0;
-        for (uint64_t it = 0; it < iters; ++it) {
+        if (AHEAD) {
+            // Two fixed register slots, the loop unrolled by two so each
+            // slot stays one register set.  The refill of the other slot
+            // goes out before this slot's CRC: the compiler's wait for this
+            // slot is then vmcnt(4) (the refill's four loads may stay in
+            // flight), and the wave keeps 4 KiB in flight while it computes.
+            StepRegs nxt;
+            // The slot's data must have landed before the refill goes out
+            // (else both slots are in flight, 8 KiB per wave, which measured
+            // slower): an empty asm reading the 16 data registers makes the
+            // compiler wait for them here.
+            auto landed = [](StepRegs &r) {
+                asm volatile("" : "+v"(r.q[0].x), "+v"(r.q[0].y), "+v"(r.q[0].z), "+v"(r.q[0].w),
+                                  "+v"(r.q[1].x), "+v"(r.q[1].y), "+v"(r.q[1].z), "+v"(r.q[1].w),
+                                  "+v"(r.q[2].x), "+v"(r.q[2].y), "+v"(r.q[2].z), "+v"(r.q[2].w),
+                                  "+v"(r.q[3].x), "+v"(r.q[3].y), "+v"(r.q[3].z), "+v"(r.q[3].w));
+            };
+            auto half = [&](uint64_t it, StepRegs &use, StepRegs &fill) {
+                if (PRIO) {
+                    rotate_prio(slot_group, it);
+                }
+                if (it == it_f) {
+                    uint32_t wl = wlast;
+                    asm volatile("" : "+v"(wl));
+                    xlast = multmodp(wl, xl);
+                }
+                landed(use);
+                issue(fill);    // unconditional: one load sequence on every path
+                if (crc_step(use)) {
+                    piece_end();
+                }
+            };
+            for (uint64_t it = 0; it < iters; it += 2) {
+                half(it, cur, nxt);
+                if (it + 1 < iters) {
+                    half(it + 1, nxt, cur);
+                }
+            }
+        }
+        for (uint64_t it = 0; !AHEAD && it < iters; ++it) {
             if (PRIO) {
                 rotate_prio(slot_group, it);
             }
@@ -1721,6 +1776,12 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
     plan_uniform(p, offs, lens, n, ph);
+    // Uniform batch of whole 4 KiB steps, 16-byte aligned: the issue-ahead
+    // stream kernel (CIO_GPU_AHEAD=0 disables).
+    p->ahead = p->unsteps != 0 && p->uh == 0 && p->uvlen % kStep == 0;
+    if (const char *r = getenv("CIO_GPU_AHEAD")) {
+        p->ahead = p->ahead && atoi(r) != 0;
+    }
     // All chunks within one wave-step (S = number of non-tiny chunks): the
     // small-chunk kernel (CIO_GPU_SMALL=0 disables).
     p->small = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
@@ -1821,8 +1882,11 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 using StreamKernel = decltype(&crc32_stream_kernel<false, 1, false>);
 
-static StreamKernel select_kernel(int prio, bool stamps, bool uniform)
+static StreamKernel select_kernel(int prio, bool stamps, bool uniform, bool ahead)
 {
+    if (ahead) {
+        return prio ? crc32_stream_kernel<false, 1, true, true> : crc32_stream_kernel<false, 0, true, true>;
+    }
     switch ((prio ? 4 : 0) + (stamps ? 2 : 0) + (uniform ? 1 : 0)) {
     case 0: return crc32_stream_kernel<false, 0, false>;
     case 1: return crc32_stream_kernel<false, 0, true>;
@@ -1868,7 +1932,7 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
         }
         return CIO_OK;
     }
-    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0);
+    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0, p->ahead && !p->stamps);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
                        p->W, p->unsteps, p->uh, p->n, p->desc, p->wstart, p->tiny,

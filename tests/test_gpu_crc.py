@@ -217,6 +217,32 @@ def test_reduced_grid_split_paths(cuda, monkeypatch, grid):
                                       po.crc_batch(buf, offs, lens, seeds=seeds), err_msg=str(k))
 
 
+@pytest.mark.parametrize("grid", [None, 3])
+def test_issue_ahead_uniform_aligned_batches(cuda, monkeypatch, grid):
+    """The issue-ahead stream kernel (uniform batches of whole 4 KiB steps at
+    16-byte-aligned offsets: two ring slots, the refill issued once the
+    current slot has landed, dummy refills past the range from the slice
+    table) against the oracle and against the one-slot kernel
+    (CIO_GPU_AHEAD=0): odd and even step counts per wave, one step per
+    wave, fewer steps than waves, chunks spanning many waves and
+    workgroups, seeds; on the full grid and a 48-wave grid (f64 split)."""
+    if grid:
+        monkeypatch.setenv("CIO_GPU_GRID", str(grid))
+    rng = np.random.default_rng(91)
+    cases = [(1, 4096 * 2), (5, 8192), (4097, 8192), (1000, 12288), (4096, 4096 * 3),
+             (3, 4096 * 4099), (300, 409600), (2, 64 << 20)]
+    for k, (n, ln) in enumerate(cases):
+        lens = np.full(n, ln, np.uint64)
+        buf, offs = wl.host_batch(0xA11E + k, lens, align=16)
+        seeds = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32) if k % 2 else None
+        want = po.crc_batch(buf, offs, lens, seeds=seeds)
+        monkeypatch.setenv("CIO_GPU_AHEAD", "1")
+        got = gpu_crc(cuda, buf, offs, lens, seeds=seeds)
+        np.testing.assert_array_equal(got, want, err_msg=f"ahead {n}x{ln}")
+        monkeypatch.setenv("CIO_GPU_AHEAD", "0")
+        np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds), want, err_msg=f"one-slot {n}x{ln}")
+
+
 def test_one_huge_chunk_spans_all_waves(cuda):
     n = 48 * 1024 * 1024 + 12345
     data = wl.gen_chunk(0xBEEF, 0, n)

@@ -16,16 +16,18 @@ step() {   # step NAME TIMEOUT CMD... : run, stop the script on any failure
   timeout -k 10 $t "$@"
   local rc=$?
   echo "[$name] rc=$rc $(python3 -c "print('%.1f s' % ($(date +%s.%N) - $t0))")" | tee -a $OUT/steps.txt
-  [ $rc -ne 0 ] && exit $rc
+  # pytest rc 1 = some tests failed (the GPU is fine): keep going; anything else stops
+  if [ $rc -ne 0 ] && ! { [ "$name" = pytest ] && [ $rc -eq 1 ]; }; then exit $rc; fi
   return 0
 }
 python3 -c "import sys; sys.path.insert(0, '.'); import bench; print('visible_gpus', bench.visible_gpus())" > $OUT/visible.txt 2>&1
 python3 -c "import torch; print('torch device_count', torch.cuda.device_count())" >> $OUT/visible.txt 2>&1
 if [ -z "${2:-}" ]; then
   step smoke 300 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.txt 2>&1"
-  step pytest 900 bash -c "python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1"
+  step pytest 900 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1"
   tail -3 $OUT/pytest_gpu.txt
 fi
+step ab_ahead 400 bash -c "python tools/ab_lib.py --libs chunkio_amd/lib/libchunkio_amd.so,chunkio_amd/lib/libchunkio_amd.so --env 'CIO_GPU_AHEAD=0|CIO_GPU_AHEAD=1' --cfg cfg2,big --iters 200 --rounds 4 > $OUT/ab_ahead.txt 2>&1"
 step bench_default 400 bash -c "python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_default.json 2> $OUT/bench_default.err"
 step spawn_n2 400 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/bench_spawn_n2.json 2> $OUT/bench_spawn_n2.err"
 step spawn_n4 500 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 4 --steps 20 --warmup 5 > $OUT/bench_spawn_n4.json 2> $OUT/bench_spawn_n4.err"
