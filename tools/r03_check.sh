@@ -4,7 +4,8 @@
 # env), the one-chunk latency crossover, and a rocprofv3 kernel trace of every
 # bench line's kernel paired with that run's own line.  Each GPU step has its
 # own time limit; the script stops at the first failure.
-# Usage (GPU box, repo root): bash tools/r03_check.sh TAG [notest] [noprof]
+# Usage (GPU box, repo root): bash tools/r03_check.sh TAG [PHASES]
+#   PHASES: comma list of test,ab,bench,spawn,cross,prof (default: all)
 set -u
 TAG=${1:-r03}
 OUT=gpurun_out/$TAG
@@ -20,19 +21,21 @@ step() {   # step NAME TIMEOUT CMD... : run, stop the script on any failure
   if [ $rc -ne 0 ] && ! { [ "$name" = pytest ] && [ $rc -eq 1 ]; }; then exit $rc; fi
   return 0
 }
+PH=",${2:-test,ab,bench,spawn,cross,prof},"
+has() { [[ "$PH" == *",$1,"* ]]; }
 python3 -c "import sys; sys.path.insert(0, '.'); import bench; print('visible_gpus', bench.visible_gpus())" > $OUT/visible.txt 2>&1
 python3 -c "import torch; print('torch device_count', torch.cuda.device_count())" >> $OUT/visible.txt 2>&1
-if [ -z "${2:-}" ]; then
+if has test; then
   step smoke 300 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.txt 2>&1"
   step pytest 900 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1"
   tail -3 $OUT/pytest_gpu.txt
 fi
-step ab_ahead 400 bash -c "python tools/ab_lib.py --libs chunkio_amd/lib/libchunkio_amd.so,chunkio_amd/lib/libchunkio_amd.so --env 'CIO_GPU_AHEAD=0|CIO_GPU_AHEAD=1' --cfg cfg2,big --iters 200 --rounds 4 > $OUT/ab_ahead.txt 2>&1"
-step bench_default 400 bash -c "python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_default.json 2> $OUT/bench_default.err"
-step spawn_n2 400 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/bench_spawn_n2.json 2> $OUT/bench_spawn_n2.err"
-step spawn_n4 500 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 4 --steps 20 --warmup 5 > $OUT/bench_spawn_n4.json 2> $OUT/bench_spawn_n4.err"
-step crossover 300 python tools/crossover.py $OUT/crossover.txt
-if [ -z "${3:-}" ]; then
+has ab && step ab_ahead 400 bash -c "python tools/ab_lib.py --libs chunkio_amd/lib/libchunkio_amd.so,chunkio_amd/lib/libchunkio_amd.so --env 'CIO_GPU_AHEAD=0|CIO_GPU_AHEAD=1' --cfg cfg2,big --iters 200 --rounds 4 > $OUT/ab_ahead.txt 2>&1"
+has bench && step bench_default 400 bash -c "python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_default.json 2> $OUT/bench_default.err"
+has spawn && step spawn_n2 400 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/bench_spawn_n2.json 2> $OUT/bench_spawn_n2.err"
+has spawn && step spawn_n4 500 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 4 --steps 20 --warmup 5 > $OUT/bench_spawn_n4.json 2> $OUT/bench_spawn_n4.err"
+has cross && step crossover 300 python tools/crossover.py $OUT/crossover.txt
+if has prof; then
   # rocprofv3 kernel traces, each of one bench line (the default line's legs, same K/W)
   for spec in "cfg2 20 5 crc32_stream_kernel 20" "cfg2 300 200 crc32_stream_kernel 100" \
               "cfg4k 200 50 crc32_small_kernel 100" "cfg4 20 5 crc32_stream_kernel 20" \
