@@ -1,16 +1,20 @@
 /*
  * crc32_host.c -- host-side CRC-32 math for libchunkio_amd.so.
  *
- *  - crc_update(): the scalar drop-in for deps/crc32/crc32.c:337-390
+ *  - crc_update(): the host drop-in for deps/crc32/crc32.c:337-390
  *    (same contract: raw state in/out, any alignment, len 0 ok, masked to
- *    32 bits).  Slice-by-16 over tables generated at load time from the
- *    reflected polynomial; used by chunkio's per-write path
- *    (src/cio_file.c:110) where a buffer is already in host cache.
+ *    32 bits).  Carry-less-multiply folding where the CPU has it (4 x 512-bit
+ *    VPCLMULQDQ accumulators from 1 KiB, 4 x 128-bit PCLMULQDQ from 64 B),
+ *    slice-by-16 over tables generated at load time from the reflected
+ *    polynomial otherwise and for short tails; used by chunkio's per-write
+ *    path (src/cio_file.c:110) where a buffer is already in host cache, and
+ *    by the chunk layer's small-batch route (crc_route.c).
  *  - GF(2) helpers: multmodp / xpow8n / shift / combine.
  *  - Generators for the device tables consumed by crc32_gpu.hip.
  */
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
 
@@ -42,13 +46,183 @@ const uint32_t *cioa_byte_table(void)
     return s16[0];
 }
 
+static uint32_t crc_update_table(uint32_t c, const unsigned char *p, size_t len);
+
+/* ---- carry-less multiply folding (x86 PCLMULQDQ / VPCLMULQDQ) -------------
+ *
+ * The reflected CRC as polynomial arithmetic: a 16-byte block loaded
+ * little-endian into a 128-bit lane has bit k <-> x^(127-k) (bit 0 of byte 0
+ * is the first message bit, the highest power).  An accumulator A (deg < 128)
+ * congruent mod P to the message so far, with the state XORed into its first
+ * four bytes, folds over D more bits as A x^D = A_hi x^(D+64) + A_lo x^D
+ * (A_hi = low qword, A_lo = high qword).  clmul of two 64-bit reflected
+ * words yields their product times x in 128-bit reflected form, so the fold
+ * constants are x^(D+63) mod P (for A_hi) and x^(D-1) mod P (for A_lo), in
+ * a 64-bit reflected word (coefficient of x^d at bit 63 - d).  At the end the
+ * 16 bytes of A are CRC'd from state 0 by the table path: crc(0, bytes of A)
+ * = A x^32 mod P, the CRC of the message.  Constants come from the same
+ * GF(2) helpers as the device tables (no magic numbers). */
+#if defined(__x86_64__)
+#include <immintrin.h>
+
+static uint64_t k_fold[4][2];    /* [D = 128, 512, 2048 (4 x 512-bit lanes), unused][lo, hi] */
+static int have_clmul, have_vclmul;
+static pthread_once_t clmul_once = PTHREAD_ONCE_INIT;
+
+/* x^n mod P for a bit count n (reflected 32-bit: bit 31 <-> x^0). */
+static uint32_t xpow_bits(uint64_t n)
+{
+    uint32_t r = 0x80000000u, sq = 0x40000000u;   /* x^0, x^1 */
+    while (n) {
+        if (n & 1u) {
+            r = cioa_multmodp(sq, r);
+        }
+        sq = cioa_multmodp(sq, sq);
+        n >>= 1;
+    }
+    return r;
+}
+
+static void build_clmul(void)
+{
+    const uint64_t d[3] = {128, 512, 2048};
+    for (int i = 0; i < 3; i++) {
+        k_fold[i][0] = (uint64_t) xpow_bits(d[i] + 63) << 32;
+        k_fold[i][1] = (uint64_t) xpow_bits(d[i] - 1) << 32;
+    }
+    __builtin_cpu_init();
+    have_clmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+    have_vclmul = have_clmul && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                  __builtin_cpu_supports("vpclmulqdq");
+}
+
+__attribute__((target("pclmul,sse4.1")))
+static inline __m128i fold128(__m128i x, __m128i k)
+{
+    return _mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11));
+}
+
+/* Bytes [0, 16 m) of p folded into one 128-bit accumulator (len >= 64). */
+__attribute__((target("pclmul,sse4.1")))
+static uint32_t crc_clmul(uint32_t c, const unsigned char *p, size_t len)
+{
+    const __m128i k128 = _mm_set_epi64x((long long) k_fold[0][1], (long long) k_fold[0][0]);
+    const __m128i k512 = _mm_set_epi64x((long long) k_fold[1][1], (long long) k_fold[1][0]);
+    __m128i x0 = _mm_loadu_si128((const __m128i *) p);
+    __m128i x1 = _mm_loadu_si128((const __m128i *) (p + 16));
+    __m128i x2 = _mm_loadu_si128((const __m128i *) (p + 32));
+    __m128i x3 = _mm_loadu_si128((const __m128i *) (p + 48));
+    x0 = _mm_xor_si128(x0, _mm_cvtsi32_si128((int) c));
+    p += 64;
+    len -= 64;
+    while (len >= 64) {
+        x0 = _mm_xor_si128(fold128(x0, k512), _mm_loadu_si128((const __m128i *) p));
+        x1 = _mm_xor_si128(fold128(x1, k512), _mm_loadu_si128((const __m128i *) (p + 16)));
+        x2 = _mm_xor_si128(fold128(x2, k512), _mm_loadu_si128((const __m128i *) (p + 32)));
+        x3 = _mm_xor_si128(fold128(x3, k512), _mm_loadu_si128((const __m128i *) (p + 48)));
+        p += 64;
+        len -= 64;
+    }
+    x1 = _mm_xor_si128(fold128(x0, k128), x1);
+    x2 = _mm_xor_si128(fold128(x1, k128), x2);
+    x3 = _mm_xor_si128(fold128(x2, k128), x3);
+    while (len >= 16) {
+        x3 = _mm_xor_si128(fold128(x3, k128), _mm_loadu_si128((const __m128i *) p));
+        p += 16;
+        len -= 16;
+    }
+    unsigned char acc[16];
+    _mm_storeu_si128((__m128i *) acc, x3);
+    return crc_update_table(crc_update_table(0, acc, 16), p, len);
+}
+
+/* The same with four 512-bit accumulators (256 bytes per iteration), then
+ * one 128-bit accumulator as above (len >= 256). */
+__attribute__((target("pclmul,sse4.1,avx512f,avx512bw,vpclmulqdq")))
+static uint32_t crc_vclmul(uint32_t c, const unsigned char *p, size_t len)
+{
+    const __m512i k2048 = _mm512_set_epi64((long long) k_fold[2][1], (long long) k_fold[2][0],
+                                           (long long) k_fold[2][1], (long long) k_fold[2][0],
+                                           (long long) k_fold[2][1], (long long) k_fold[2][0],
+                                           (long long) k_fold[2][1], (long long) k_fold[2][0]);
+    __m512i y0 = _mm512_loadu_si512((const void *) p);
+    __m512i y1 = _mm512_loadu_si512((const void *) (p + 64));
+    __m512i y2 = _mm512_loadu_si512((const void *) (p + 128));
+    __m512i y3 = _mm512_loadu_si512((const void *) (p + 192));
+    y0 = _mm512_xor_si512(y0, _mm512_zextsi128_si512(_mm_cvtsi32_si128((int) c)));
+    p += 256;
+    len -= 256;
+    while (len >= 256) {
+#define CIOA_FOLD512(y, off)                                                                         \
+        y = _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(y, k2048, 0x00),                      \
+                                      _mm512_clmulepi64_epi128(y, k2048, 0x11),                      \
+                                      _mm512_loadu_si512((const void *) (p + (off))), 0x96)
+        CIOA_FOLD512(y0, 0);
+        CIOA_FOLD512(y1, 64);
+        CIOA_FOLD512(y2, 128);
+        CIOA_FOLD512(y3, 192);
+#undef CIOA_FOLD512
+        p += 256;
+        len -= 256;
+    }
+    /* The 16 lanes of y0..y3 are 16 consecutive 16-byte blocks: fold them in
+     * order into one 128-bit accumulator. */
+    const __m128i k128 = _mm_set_epi64x((long long) k_fold[0][1], (long long) k_fold[0][0]);
+    __m128i lanes[16];
+    _mm512_storeu_si512((void *) &lanes[0], y0);
+    _mm512_storeu_si512((void *) &lanes[4], y1);
+    _mm512_storeu_si512((void *) &lanes[8], y2);
+    _mm512_storeu_si512((void *) &lanes[12], y3);
+    __m128i x = lanes[0];
+    for (int i = 1; i < 16; i++) {
+        x = _mm_xor_si128(fold128(x, k128), lanes[i]);
+    }
+    while (len >= 16) {
+        x = _mm_xor_si128(fold128(x, k128), _mm_loadu_si128((const __m128i *) p));
+        p += 16;
+        len -= 16;
+    }
+    unsigned char acc[16];
+    _mm_storeu_si128((__m128i *) acc, x);
+    return crc_update_table(crc_update_table(0, acc, 16), p, len);
+}
+#endif
+
+/* CIOA_HOST_CRC=table forces the table path (A/B and tests). */
+static int host_crc_mode(void)
+{
+    static int mode = -1;
+    if (mode < 0) {
+        const char *r = getenv("CIOA_HOST_CRC");
+        mode = (r && strcmp(r, "table") == 0) ? 0 : (r && strcmp(r, "clmul") == 0) ? 1 : 2;
+    }
+    return mode;
+}
+
 uint64_t cioa_crc_update_host(uint64_t crc, const void *data, size_t len)
 {
     const unsigned char *p = (const unsigned char *) data;
     uint32_t c = (uint32_t) crc;
 
     pthread_once(&s16_once, build_s16);
+#if defined(__x86_64__)
+    if (len >= 64) {
+        pthread_once(&clmul_once, build_clmul);
+        const int mode = host_crc_mode();
+        if (mode == 2 && have_vclmul && len >= 1024) {
+            return (uint64_t) crc_vclmul(c, p, len);
+        }
+        if (mode >= 1 && have_clmul) {
+            return (uint64_t) crc_clmul(c, p, len);
+        }
+    }
+#endif
+    return (uint64_t) crc_update_table(c, p, len);
+}
 
+/* Slice-by-16 over the s16 tables (built by the caller). */
+static uint32_t crc_update_table(uint32_t c, const unsigned char *p, size_t len)
+{
     while (len && ((uintptr_t) p & 15u)) {
         c = s16[0][(c ^ *p++) & 0xffu] ^ (c >> 8);
         len--;
@@ -74,7 +248,7 @@ uint64_t cioa_crc_update_host(uint64_t crc, const void *data, size_t len)
     while (len--) {
         c = s16[0][(c ^ *p++) & 0xffu] ^ (c >> 8);
     }
-    return (uint64_t) c;
+    return c;
 }
 
 /* a(x)*b(x) mod P(x); bit 31 carries the x^0 coefficient (reflected). */
