@@ -1438,6 +1438,70 @@ fill_kernel(uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     }
 }
 
+// Diagnostic (CIO_GPU_RS_DYN="pool_permille,U,NC"): the read-only stream with
+// a dynamic tail.  The first S - P steps are split evenly over the waves as
+// in read_stream_kernel; the last P steps form a pool of U-step units, dealt
+// over NC counters (one cache line each).  A wave that has finished its
+// static range claims units from the counter its workgroup's XCD and slot
+// hash to, moving on to the next counter when one is exhausted, so waves on
+// fast CUs take over work that slow CUs would otherwise finish late.  The
+// next unit is claimed before the current one is streamed (one returning
+// atomic in flight).  Counters are zeroed by the host before each launch.
+__global__ void __launch_bounds__(kThreads, 1)
+read_stream_dyn_kernel(const uint8_t *__restrict__ base, uint64_t S, uint64_t Sst, uint32_t U,
+                       uint32_t *__restrict__ ctr, uint32_t NC, uint32_t upc, uint32_t npool,
+                       uint32_t *__restrict__ sink)
+{
+    const uint32_t W = gridDim.x * (kThreads / kWave);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6));
+    const uint32_t lane = threadIdx.x & 63u;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    auto step = [&](uint64_t g) {
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(base + g * kStep + (uint64_t) lane * kGran);
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+            acc ^= __builtin_nontemporal_load(p + q * kWave);
+        }
+    };
+    const uint64_t g0 = wave_start(wave, Sst, W), g1 = wave_start((uint64_t) wave + 1, Sst, W);
+    for (uint64_t g = g0; g < g1; ++g) {
+        step(g);
+    }
+    uint32_t c = ((blockIdx.x & 7u) * (NC / 8u) + ((threadIdx.x >> 6) % (NC / 8u))) % NC;
+    uint32_t tries = 0;
+    auto claim = [&](uint32_t cc) -> uint32_t {
+        uint32_t u = 0;
+        if (lane == 0) {
+            u = __hip_atomic_fetch_add(&ctr[cc * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return __builtin_amdgcn_readfirstlane(u);
+    };
+    uint32_t u = claim(c);
+    while (tries < NC) {
+        if (u >= upc) {
+            c = (c + 1u) % NC;
+            ++tries;
+            u = claim(c);
+            continue;
+        }
+        const uint32_t unit = c * upc + u;
+        const uint32_t cur_c = c;
+        (void) cur_c;
+        u = claim(c);    // the next claim in flight while this unit streams
+        if (unit < npool) {
+            const uint64_t a = Sst + (uint64_t) unit * U;
+            const uint64_t b = min(S, a + U);
+            for (uint64_t g = a; g < b; ++g) {
+                step(g);
+            }
+        }
+    }
+    const uint32_t x = wave_xor(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]);
+    if (lane == 0) {
+        sink[wave] = x;
+    }
+}
+
 // ---------------------------------------------------------------- host side
 
 }  // namespace
@@ -2017,7 +2081,22 @@ int cioa_debug_rs_stamps(unsigned long long *host, size_t cap)
     return (int) g_rs_waves;
 }
 
+static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, hipEvent_t ev0, hipEvent_t ev1);
+
 int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
+{
+    return read_stream_impl(dev_base, bytes, stream, nullptr, nullptr);
+}
+
+/* Diagnostic (not in the public header): the read-only stream with events
+ * recorded right around its kernel (after the dynamic-tail counter reset). */
+int cioa_debug_read_stream_events(const void *dev_base, uint64_t bytes, void *stream, void *ev0, void *ev1)
+{
+    return read_stream_impl(dev_base, bytes, stream, reinterpret_cast<hipEvent_t>(ev0),
+                            reinterpret_cast<hipEvent_t>(ev1));
+}
+
+static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, hipEvent_t ev0, hipEvent_t ev1)
 {
     DeviceState *st;
     if (device_state(&st) != CIO_OK) {
@@ -2054,10 +2133,42 @@ int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
         const int lb = atoi(r);
         work |= (lb == 64 ? 2u : lb == 32 ? 1u : 0u) << 16;
     }
+    if (const char *r = getenv("CIO_GPU_RS_DYN")) {
+        unsigned pm = 0, U = 4, NC = 64;
+        if (sscanf(r, "%u,%u,%u", &pm, &U, &NC) >= 1 && pm > 0 && pm <= 1000 && U >= 1 && NC >= 8 &&
+            NC <= 1024 && NC % 8 == 0) {
+            static thread_local uint32_t *ctr = nullptr;
+            if (!ctr) {
+                HIP_TRY(hipMalloc(&ctr, 1024 * 32 * sizeof(uint32_t)), "read_stream: hipMalloc");
+            }
+            const uint64_t P = S * pm / 1000;
+            const uint64_t npool = (P + U - 1) / U;
+            const uint32_t upc = (uint32_t) ((npool + NC - 1) / NC);
+            hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+            HIP_TRY(hipMemsetAsync(ctr, 0, (size_t) NC * 32 * sizeof(uint32_t), hs), "read_stream: memset");
+            if (ev0) {
+                HIP_TRY(hipEventRecord(ev0, hs), "hipEventRecord");
+            }
+            hipLaunchKernelGGL(read_stream_dyn_kernel, dim3(st->cus), dim3(kThreads), 0, hs,
+                               reinterpret_cast<const uint8_t *>(dev_base), S, S - P, (uint32_t) U, ctr,
+                               (uint32_t) NC, upc, (uint32_t) npool, sink);
+            HIP_TRY(hipGetLastError(), "read_stream_dyn_kernel launch");
+            if (ev1) {
+                HIP_TRY(hipEventRecord(ev1, hs), "hipEventRecord");
+            }
+            return CIO_OK;
+        }
+    }
+    if (ev0) {
+        HIP_TRY(hipEventRecord(ev0, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
+    }
     hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream),
                        reinterpret_cast<const uint8_t *>(dev_base), S, sink, B, stamps, work);
     HIP_TRY(hipGetLastError(), "read_stream_kernel launch");
+    if (ev1) {
+        HIP_TRY(hipEventRecord(ev1, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
+    }
     return CIO_OK;
 }
 

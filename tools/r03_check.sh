@@ -5,7 +5,7 @@
 # bench line's kernel paired with that run's own line.  Each GPU step has its
 # own time limit; the script stops at the first failure.
 # Usage (GPU box, repo root): bash tools/r03_check.sh TAG [PHASES]
-#   PHASES: comma list of test,ab,bench,spawn,cross,prof (default: all)
+#   PHASES: comma list of test,ab,bench,spawn,cross,rsdyn,prof (default: all but rsdyn)
 set -u
 TAG=${1:-r03}
 OUT=gpurun_out/$TAG
@@ -35,6 +35,7 @@ has bench && step bench_default 400 bash -c "python bench.py --gpus 1 --steps 20
 has spawn && step spawn_n2 400 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/bench_spawn_n2.json 2> $OUT/bench_spawn_n2.err"
 has spawn && step spawn_n4 500 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 4 --steps 20 --warmup 5 > $OUT/bench_spawn_n4.json 2> $OUT/bench_spawn_n4.err"
 has cross && step crossover 300 python tools/crossover.py $OUT/crossover.txt
+has rsdyn && step rs_dyn 300 bash -c "python tools/rs_dyn_probe.py 4 > $OUT/rs_dyn_probe.txt 2>&1"
 if has prof; then
   # rocprofv3 kernel traces, each of one bench line (the default line's legs, same K/W)
   for spec in "cfg2 20 5 crc32_stream_kernel 20" "cfg2 300 200 crc32_stream_kernel 100" \
