@@ -35,7 +35,8 @@ has bench && step bench_default 400 bash -c "python bench.py --gpus 1 --steps 20
 has spawn && step spawn_n2 400 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/bench_spawn_n2.json 2> $OUT/bench_spawn_n2.err"
 has spawn && step spawn_n4 500 bash -c "CIO_BENCH_REHEARSE=1 python bench.py --gpus 4 --steps 20 --warmup 5 > $OUT/bench_spawn_n4.json 2> $OUT/bench_spawn_n4.err"
 has cross && step crossover 300 python tools/crossover.py $OUT/crossover.txt
-has rsdyn && step rs_dyn 300 bash -c "python tools/rs_dyn_probe.py 4 > $OUT/rs_dyn_probe.txt 2>&1"
+has rsdyn && step rs_dyn 300 bash -c "python tools/rs_dyn_probe.py 4 '${RSDYN:-static;100,4,64;150,4,64;200,4,64;150,2,64;150,8,64;150,4,256;300,4,64}' > $OUT/rs_dyn_probe.txt 2>&1"
+has pmc4k && step pmc_cfg4k 300 bash tools/pmc_configs.sh cfg4k
 if has prof; then
   # rocprofv3 kernel traces, each of one bench line (the default line's legs, same K/W)
   for spec in "cfg2 20 5 crc32_stream_kernel 20" "cfg2 300 200 crc32_stream_kernel 100" \

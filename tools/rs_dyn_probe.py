@@ -2,7 +2,7 @@
 """Does a dynamic tail recover the per-CU finish spread of the read-only
 stream?  (Go/no-go for dynamic balancing in the CRC kernel.)
 
-    python tools/rs_dyn_probe.py [rounds]
+    python tools/rs_dyn_probe.py [rounds] ["static;100,4,64;..."]
 
 Over the cfg2 batch (1024 x 409,600 B, 4 rotating buffers): the static
 read-only stream (read_stream_kernel, the CRC kernel's split) against
@@ -36,7 +36,9 @@ def main():
     for b, t in enumerate(bufs):
         cio.fill_synthetic(t, offs, lens, 0x11 + b)
     sp = torch.cuda.current_stream().cuda_stream
-    variants = ["", "100,4,64", "150,4,64", "200,4,64", "150,2,64", "150,8,64", "150,4,256", "300,4,64"]
+    variants = (sys.argv[2].split(";") if len(sys.argv) > 2 else
+                ["", "100,4,64", "150,4,64", "200,4,64", "150,2,64", "150,8,64", "150,4,256", "300,4,64"])
+    variants = ["" if v == "static" else v for v in variants]
     res = {v: [] for v in variants}
     n = 100
     for r in range(rounds):
