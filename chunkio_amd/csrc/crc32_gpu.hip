@@ -180,6 +180,17 @@ __device__ __forceinline__ uint64_t wave_start(uint64_t w, uint64_t S, uint64_t 
     return split_point(w, S, W);
 }
 
+// Replicas the lookups use: 32 slice / 8 shift.  Diagnostic build
+// (-DCIO_DIAG_HALF_REPLICAS): lanes read only 16 slice and 4 shift replicas
+// -- the tables a workgroup would hold in half the LDS (80 KiB, two
+// workgroups per CU) -- so every lookup group of 32 lanes takes the 2-way
+// bank conflicts such a layout has, at the current occupancy.
+#ifdef CIO_DIAG_HALF_REPLICAS
+constexpr uint32_t kSliceRepMask = 15u, kShiftRepMask = 3u;
+#else
+constexpr uint32_t kSliceRepMask = 31u, kShiftRepMask = 7u;
+#endif
+
 // Slice tables in LDS, replicated 32x so lane l always reads bank (l & 31):
 //   byte address(k, b, lane) = (k>>1)*65536 + b*256 + (k&1)*128 + (lane&31)*4
 // One v_perm_b32 builds the address: {0, k>>1, x.byte, lane*4}.  lbase_hi =
@@ -583,9 +594,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
     const uint32_t lane = tid & 63u;
-    const uint32_t lb_lo = (lane & 31u) << 2;
+    const uint32_t lb_lo = (lane & kSliceRepMask) << 2;
     const uint32_t lb_hi = lb_lo | 0x10000u;
-    const uint32_t lrep = (lane & 7u) << 2;
+    const uint32_t lrep = (lane & kShiftRepMask) << 2;
     const uint32_t slot_group = __builtin_amdgcn_readfirstlane((tid >> 6) >> 2);
     const uint64_t g0 = uniform_u64(wave_start(wave, S, W));
     const uint64_t gend = uniform_u64(wave_start((uint64_t) wave + 1, S, W));
@@ -1082,9 +1093,9 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / kWave) + (tid >> 6));
     const uint32_t lane = tid & 63u;
-    const uint32_t lb_lo = (lane & 31u) << 2;
+    const uint32_t lb_lo = (lane & kSliceRepMask) << 2;
     const uint32_t lb_hi = lb_lo | 0x10000u;
-    const uint32_t lrep = (lane & 7u) << 2;
+    const uint32_t lrep = (lane & kShiftRepMask) << 2;
     const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t) split_point(wave, n, W));
     const uint32_t c1 = __builtin_amdgcn_readfirstlane((uint32_t) split_point((uint64_t) wave + 1, n, W));
     const uint32_t lbyte = lane * kGran;

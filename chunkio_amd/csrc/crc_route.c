@@ -11,9 +11,15 @@
  * drop-in for deps/crc32/crc32.c:337-390) on the calling thread finishes
  * first.  cioa_crc_batch_route() sends a batch whose total size is at most
  * cio_crc32_cpu_max() bytes there, and everything larger to the GPU.  The
- * default comes from the latency table in profiles/r03/crossover_*.txt
- * (tools/crossover.py: one-chunk GPU host batch against crc_update, 16 B to
- * 8 MiB, on the GPU box).  Results are identical either way (both compute
+ * default comes from the latency table in profiles/r03/crossover_r03b.txt
+ * (tools/crossover.py on the GPU box): one chunk through the GPU host batch
+ * costs 85 us at any size up to 4 KiB and 206 us at 2 MiB (its fixed cost,
+ * then ~20 GB/s), while crc_update (VPCLMULQDQ folding, crc32_host.c) takes
+ * 0.3 us at 16 B and 27 us at 2 MiB (~77 GB/s on cached data), so a single
+ * chunk never pays for the round trip up to 8 MiB.  A batch of many chunks
+ * streams through the pipelined GPU path at ~50 GB/s (PCIe-bound) against
+ * one host thread's ~25 GB/s from DRAM: 85 us + B / 50 GB/s < B / 25 GB/s
+ * from B ~ 4 MiB.  Results are identical either way (both compute
  * crc_update(seed, bytes)); the public cio_crc32_batch_* entry points never
  * route -- they are the GPU path.
  */
@@ -29,7 +35,7 @@
 
 /* Bytes per call at or below which the host CRC is faster than a GPU round
  * trip (measured; see the header comment). */
-#define CIOA_CPU_CRC_MAX_DEFAULT ((size_t) 256 << 10)
+#define CIOA_CPU_CRC_MAX_DEFAULT ((size_t) 4 << 20)
 
 static size_t g_cpu_max;
 static int g_cpu_max_set;
