@@ -523,6 +523,13 @@ def run_e2e(args, rank, world, device, dist):
         barrier(dist)
         elapsed_reg = max_over_ranks(time.perf_counter() - t0, dist, device)
         legs_reg = cio.pipe_last_timing()
+        # the DMA engine's rate from the registered pages themselves (the
+        # registered path's ceiling), beside pinned_h2d_GBps in `breakdown`
+        import ctypes
+        f_h2d = cio.lib().cioa_debug_h2d_gbps
+        f_h2d.restype = ctypes.c_double
+        f_h2d.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        reg_h2d = round(f_h2d(host.ctypes.data, host.size, 5), 2)
     finally:
         cio.host_unregister(host)
     value_reg = int(lens.sum()) * world * steps / elapsed_reg / 1e9
@@ -541,6 +548,7 @@ def run_e2e(args, rank, world, device, dist):
             "registered_in_place": {"value": round(value_reg, 3), "unit": "GB/s",
                                     "ms_per_step": round(elapsed_reg / steps * 1e3, 4),
                                     "register_ms_once": round(reg_ms, 2),
+                                    "h2d_from_registered_pages_GBps": reg_h2d,
                                     "note": "host batch pinned once with cio_crc32_host_register "
                                             "(outside the timed loop); chunks DMA'd directly"},
             "breakdown": e2e_breakdown(host, device),

@@ -885,6 +885,42 @@ extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t 
                        "cio_crc32_batch_host_multi");
 }
 
+/* Diagnostic (not in the public header): the H2D DMA rate from `host`
+ * (pinned, registered or pageable) into a device buffer, `reps` copies of
+ * `bytes` on one stream; GB/s, or a negative value on error.  bench.py puts
+ * it beside the registered-in-place E2E rate: registration pins the
+ * caller's own (4 KiB) pages, and the engine's rate from them is the
+ * registered path's real ceiling. */
+extern "C" double cioa_debug_h2d_gbps(const void *host, size_t bytes, int reps)
+{
+    void *d = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    double r = -1.0;
+    if (!host || bytes == 0 || reps <= 0 || hipMalloc(&d, bytes) != hipSuccess) {
+        return -1.0;
+    }
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+        hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+        hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess && hipEventRecord(e0, s) == hipSuccess) {
+        bool ok = true;
+        for (int i = 0; i < reps && ok; i++) {
+            ok = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+        }
+        float ms = 0.f;
+        if (ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+            hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f) {
+            r = (double) bytes * reps / (ms * 1e-3) / 1e9;
+        }
+    }
+    if (e0) (void) hipEventDestroy(e0);
+    if (e1) (void) hipEventDestroy(e1);
+    if (s) (void) hipStreamDestroy(s);
+    (void) hipFree(d);
+    return r;
+}
+
 extern "C" int cio_gpu_pipe_last_timing(double *out, int n)
 {
     if (!out || n <= 0) {
