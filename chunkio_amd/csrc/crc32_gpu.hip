@@ -1851,12 +1851,18 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
     plan_uniform(p, offs, lens, n, ph);
-    // Uniform batch of whole 4 KiB steps, 16-byte aligned: the issue-ahead
-    // stream kernel (CIO_GPU_AHEAD=0 disables).
+    // Uniform batch of whole 4 KiB steps, 16-byte aligned, with short wave
+    // ranges (<= 64 steps, e.g. cfg2's 25): the issue-ahead stream kernel.
+    // Interleaved A/Bs (profiles/r03/ab_issue_ahead_*.txt): cfg2 -0.6 to
+    // -1.8 %, 100- and 256-step ranges -0.3 to +0.6 % (neutral), so only
+    // short ranges, where the first steps' start-up is a larger share, take
+    // it.  CIO_GPU_AHEAD=1 forces it for any uniform aligned batch, 0 never.
     p->ahead = p->unsteps != 0 && p->uh == 0 && p->uvlen % kStep == 0;
+    bool short_ranges = p->S <= 64ull * p->W;
     if (const char *r = getenv("CIO_GPU_AHEAD")) {
-        p->ahead = p->ahead && atoi(r) != 0;
+        short_ranges = atoi(r) != 0;
     }
+    p->ahead = p->ahead && short_ranges;
     // All chunks within one wave-step (S = number of non-tiny chunks): the
     // small-chunk kernel (CIO_GPU_SMALL=0 disables).
     p->small = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
