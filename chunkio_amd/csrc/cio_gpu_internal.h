@@ -112,6 +112,7 @@ struct cio_crc32_plan {
     uint32_t unsteps = 0, uh = 0;
     bool small = false;        // every chunk fits one wave-step: crc32_small_kernel
     bool ahead = false;        // uniform, 16-B aligned, whole 4 KiB steps: issue-ahead stream kernel
+    bool l64 = false;          // issue-ahead kernel with one 64-byte chain per lane (CIO_GPU_L64)
     unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     cioa::ChunkDesc *desc = nullptr;

@@ -378,6 +378,48 @@ __device__ __forceinline__ void load_step(StepRegs &r, const uint8_t *cbase, uin
     }
 }
 
+// L64 layout (issue-ahead kernel only): lane L = 16 g + i owns the 64
+// contiguous bytes [64 L, 64 L + 64) of a step, one chain per lane.  Each of
+// the 4 loads still reads one whole 1 KiB row (fully coalesced): row r's
+// instruction gives lane (g, i) the block 4 i + g of row r.  As a 4 x 4
+// matrix of 16-lane blocks (register r, lane group g) the rows then sit
+// transposed; two butterfly stages of in-register swaps -- permlane16_swap
+// (groups g ^ 1 between registers r, r ^ 1) and permlane32_swap (groups g ^ 2
+// between registers r, r ^ 2) -- give every owner lane its 4 blocks in
+// order: register k = bytes 64 L + 16 k.  16 swaps per step replace the 3
+// extra 4-lookup shifts of the 4-sub-chain layout (68 LDS lookups per step
+// instead of 80) and the piece-end Horner fold.
+__device__ __forceinline__ void load_step64(StepRegs &r, const uint8_t *cbase, uint64_t jj, uint32_t lane)
+{
+    const uint64_t b0 = jj * kStep + (uint64_t) (64u * (lane & 15u) + 16u * (lane >> 4));
+#pragma unroll
+    for (int q = 0; q < kSub; ++q) {
+        r.q[q] = ldg16(cbase + b0 + (uint64_t) q * kRow);
+    }
+}
+
+__device__ __forceinline__ void swap16(uint32_t &a, uint32_t &b)
+{
+    const auto t = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = t[0];
+    b = t[1];
+}
+
+__device__ __forceinline__ void swap32(uint32_t &a, uint32_t &b)
+{
+    const auto t = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = t[0];
+    b = t[1];
+}
+
+__device__ __forceinline__ void transpose64(StepRegs &r)
+{
+    swap16(r.q[0].x, r.q[1].x); swap16(r.q[0].y, r.q[1].y); swap16(r.q[0].z, r.q[1].z); swap16(r.q[0].w, r.q[1].w);
+    swap16(r.q[2].x, r.q[3].x); swap16(r.q[2].y, r.q[3].y); swap16(r.q[2].z, r.q[3].z); swap16(r.q[2].w, r.q[3].w);
+    swap32(r.q[0].x, r.q[2].x); swap32(r.q[0].y, r.q[2].y); swap32(r.q[0].z, r.q[2].z); swap32(r.q[0].w, r.q[2].w);
+    swap32(r.q[1].x, r.q[3].x); swap32(r.q[1].y, r.q[3].y); swap32(r.q[1].z, r.q[3].z); swap32(r.q[1].w, r.q[3].w);
+}
+
 // Generic step: partial blocks at a chunk end, and the first step of a chunk
 // (alignment-head zeroing + seed fold into content bytes 0..3, which can
 // straddle lanes 0 and 1 of sub-chain 0).
@@ -572,7 +614,7 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 // the next step's loads are issued as soon as this step's data has landed,
 // BEFORE its CRC -- still one step (4 KiB) in flight per wave, as in the
 // read-only stream, but no longer none while the wave computes.
-template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false, bool AHEAD = false>
+template <bool STAMPS = false, int PRIO = 1, bool UNIFORM = false, bool AHEAD = false, bool L64 = false>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t ua0, uint64_t uvlen,
                     uint32_t W, uint32_t unsteps, uint32_t uh, uint32_t n,
@@ -654,7 +696,11 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         if (AHEAD) {
             const bool real = nload > 0;
             const uint8_t *src = real ? lbase + ld.a : reinterpret_cast<const uint8_t *>(g_slice);
-            load_step(r, src, real ? lj : 0, real ? ld.vlen : (uint64_t) kStep, lane);
+            if (L64) {
+                load_step64(r, src, real ? lj : 0, lane);
+            } else {
+                load_step(r, src, real ? lj : 0, real ? ld.vlen : (uint64_t) kStep, lane);
+            }
         } else {
         const uint64_t jj = nload > 0 ? lj : (uint64_t) ld.nsteps - 1;
         load_step(r, lbase + ld.a, jj, ld.vlen, lane);
@@ -704,7 +750,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // the piece end.  The 1024 (3 - q) parts are compile-time constants
     // (fold_full); the lane part x^(8 * 16 (63 - l)) is fetched once here
     // instead of gathered from g_x8 at every piece end.
-    const uint32_t xl = g_x8[kRow - (lane + 1) * kGran];
+    const uint32_t xl = g_x8[L64 ? 64u * (63u - lane) : kRow - (lane + 1) * kGran];
     // Workgroup-local fold.  A split chunk whose pieces all lie in this
     // workgroup's 16 waves skips the partial slot and the arrival counter:
     // each non-final piece (a wave's last piece) goes to the wave's LDS word
@@ -735,7 +781,8 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t idx = tid + (uint32_t) kThreads * e;
-        table_entries(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u, tab_v[e], tab_sv[e]);
+        table_entries<L64 ? cx_xpow8n(kStep - 64) : kXStepShift>(__builtin_amdgcn_readfirstlane(idx >> 8),
+                                                                 idx & 255u, tab_v[e], tab_sv[e]);
     }
     write_tables<STAMPS>(lds, tid, tab_v, tab_sv, t_wt);
     __syncthreads();
@@ -756,7 +803,20 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // step's loads are issued, so their latency overlaps the fold.
         auto crc_step = [&](StepRegs &r) -> bool {
             {
-                if (AHEAD || j < full_end) {
+                if (L64) {
+                    // one chain per lane: jump 4032 bytes, then 64 contiguous bytes
+                    const uint32_t h0 = step_shift(lds, lrep, s[0]);
+                    transpose64(r);
+                    if (j == 0) {
+                        r.q[0].x ^= lane == 0 ? seed : 0u;   // h = 0: the seed on content bytes 0..3
+                    }
+                    uint32_t st = block16(lds, lb_lo, lb_hi, h0, r.q[0]);
+#pragma unroll
+                    for (int q = 1; q < kSub; ++q) {
+                        st = block16(lds, lb_lo, lb_hi, st, r.q[q]);
+                    }
+                    s[0] = st;
+                } else if (AHEAD || j < full_end) {
                     // The 4080-byte jump of every sub-chain needs only its
                     // state: its lookups go out before the first use of the
                     // step's data, so after the data lands only the four
@@ -803,7 +863,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         // of the lane factor, landing at the chunk end.
                         uint32_t a = j < d.nsteps ? xlast : xl;
                         asm volatile("" : "+v"(a));
-                        contrib = multmodp(a, fold_full<UNIFORM>(s));
+                        contrib = multmodp(a, L64 ? s[0] : fold_full<UNIFORM>(s));
                     } else {
                         const uint64_t pend = min(j * kStep, d.vlen);
                         contrib = 0;
@@ -1863,6 +1923,9 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         short_ranges = atoi(r) != 0;
     }
     p->ahead = p->ahead && short_ranges;
+    if (const char *r = getenv("CIO_GPU_L64")) {
+        p->l64 = atoi(r) != 0;
+    }
     // All chunks within one wave-step (S = number of non-tiny chunks): the
     // small-chunk kernel (CIO_GPU_SMALL=0 disables).
     p->small = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
@@ -1963,9 +2026,13 @@ int cio_crc32_plan_exec(const cio_crc32_plan *p, const void *dev_base, const uin
 
 using StreamKernel = decltype(&crc32_stream_kernel<false, 1, false>);
 
-static StreamKernel select_kernel(int prio, bool stamps, bool uniform, bool ahead)
+static StreamKernel select_kernel(int prio, bool stamps, bool uniform, bool ahead, bool l64)
 {
     if (ahead) {
+        if (l64) {
+            return prio ? crc32_stream_kernel<false, 1, true, true, true>
+                        : crc32_stream_kernel<false, 0, true, true, true>;
+        }
         return prio ? crc32_stream_kernel<false, 1, true, true> : crc32_stream_kernel<false, 0, true, true>;
     }
     switch ((prio ? 4 : 0) + (stamps ? 2 : 0) + (uniform ? 1 : 0)) {
@@ -2013,7 +2080,7 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
         }
         return CIO_OK;
     }
-    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0, p->ahead && !p->stamps);
+    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0, p->ahead && !p->stamps, p->l64);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
                        p->W, p->unsteps, p->uh, p->n, p->desc, p->wstart, p->tiny,

@@ -217,8 +217,9 @@ def test_reduced_grid_split_paths(cuda, monkeypatch, grid):
                                       po.crc_batch(buf, offs, lens, seeds=seeds), err_msg=str(k))
 
 
+@pytest.mark.parametrize("l64", ["0", "1"])
 @pytest.mark.parametrize("grid", [None, 3])
-def test_issue_ahead_uniform_aligned_batches(cuda, monkeypatch, grid):
+def test_issue_ahead_uniform_aligned_batches(cuda, monkeypatch, grid, l64):
     """The issue-ahead stream kernel (uniform batches of whole 4 KiB steps at
     16-byte-aligned offsets: two ring slots, the refill issued once the
     current slot has landed, dummy refills past the range from the slice
@@ -228,6 +229,7 @@ def test_issue_ahead_uniform_aligned_batches(cuda, monkeypatch, grid):
     workgroups, seeds; on the full grid and a 48-wave grid (f64 split)."""
     if grid:
         monkeypatch.setenv("CIO_GPU_GRID", str(grid))
+    monkeypatch.setenv("CIO_GPU_L64", l64)        # one 64-byte chain per lane (permlane transpose)
     rng = np.random.default_rng(91)
     cases = [(1, 4096 * 2), (5, 8192), (4097, 8192), (1000, 12288), (4096, 4096 * 3),
              (3, 4096 * 4099), (300, 409600), (2, 64 << 20)]

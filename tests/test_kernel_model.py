@@ -198,3 +198,60 @@ def test_plan_workgroup_local_fold_flags(W, kind):
         # 100-step chunks, 25 steps per wave: every chunk is split over 4
         # waves of one workgroup.
         assert n_fold == 1024 and n_pub == 3 * 1024
+
+
+# ---- L64 layout (issue-ahead kernel, CIO_GPU_L64): one chain per lane -------
+
+def _permlane16_swap(a, b):
+    """v_permlane16_swap_b32 a, b: odd 16-lane rows of a <-> even rows of b."""
+    a, b = a.copy(), b.copy()
+    for r in (0, 2):
+        lo, hi = slice(16 * r, 16 * r + 16), slice(16 * (r + 1), 16 * (r + 2))
+        a[hi], b[lo] = b[lo].copy(), a[hi].copy()
+    return a, b
+
+
+def _permlane32_swap(a, b):
+    """v_permlane32_swap_b32 a, b: lanes 32..63 of a <-> lanes 0..31 of b."""
+    a, b = a.copy(), b.copy()
+    a[32:], b[:32] = b[:32].copy(), a[32:].copy()
+    return a, b
+
+
+def test_l64_transpose_gives_each_lane_64_contiguous_bytes():
+    """Row r's load gives lane (g, i) = 16 g + i the block 4 i + g of row r;
+    the two butterfly stages of load_step64/transpose64 then leave register
+    k of lane L holding step bytes [64 L + 16 k, +16).  Modelled on block
+    indices (one 'dword' per block)."""
+    lane = np.arange(64)
+    regs = [r * 64 + 4 * (lane & 15) + (lane >> 4) for r in range(4)]   # block index in the step
+    regs[0], regs[1] = _permlane16_swap(regs[0], regs[1])
+    regs[2], regs[3] = _permlane16_swap(regs[2], regs[3])
+    regs[0], regs[2] = _permlane32_swap(regs[0], regs[2])
+    regs[1], regs[3] = _permlane32_swap(regs[1], regs[3])
+    for k in range(4):
+        np.testing.assert_array_equal(regs[k], 4 * lane + k)
+    # every load instruction still reads one whole 1 KiB row
+    for r in range(4):
+        offs = r * 1024 + 64 * (lane & 15) + 16 * (lane >> 4)
+        assert sorted(offs.tolist()) == list(range(r * 1024, r * 1024 + 1024, 16))
+
+
+@pytest.mark.parametrize("nsteps,seed", [(1, INIT), (3, 0x1234ABCD), (25, INIT)])
+def test_l64_chain_decomposition(nsteps, seed):
+    """One chain per lane over [64 L, 64 L + 64) of every step, a 4032-byte
+    shift between steps, the seed on content bytes 0..3, the piece end
+    reached by x^(8 * 64 (63 - L)) and an XOR over the wave: equals
+    crc_update over the whole (aligned, whole-step) chunk."""
+    rng = np.random.default_rng(nsteps)
+    data = rng.integers(0, 256, nsteps * STEP, dtype=np.uint8)
+    acc = 0
+    for L in range(WAVE):
+        s = 0
+        for j in range(nsteps):
+            blk = data[j * STEP + 64 * L: j * STEP + 64 * L + 64].copy()
+            if j == 0 and L == 0:
+                blk[:4] ^= np.frombuffer(int(seed).to_bytes(4, "little"), np.uint8)
+            s = po.crc_update(po.crc_shift(s, STEP - 64), blk)
+        acc ^= po.crc_shift(s, 64 * (63 - L))
+    assert acc == po.crc_update(seed, data)
