@@ -1138,7 +1138,11 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <bool UNI, bool SEEDS>
+// L64 (CIO_GPU_L64): the stream kernel's L64 layout (load_step64 /
+// transpose64): lane L owns bytes [64 L, 64 L + 64) of the chunk, so its
+// chain runs through 64 contiguous bytes with no jump at all (64 lookups per
+// chunk instead of 76) and folds with x^(8 * 64 (63 - L)).
+template <bool UNI, bool SEEDS, bool L64 = false>
 __global__ void __launch_bounds__(kThreads, 1)
 crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t uvlen, uint32_t uh,
                    uint32_t W, uint32_t n, uint32_t ntiny, const uint32_t *__restrict__ g_x8,
@@ -1159,6 +1163,8 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t) split_point(wave, n, W));
     const uint32_t c1 = __builtin_amdgcn_readfirstlane((uint32_t) split_point((uint64_t) wave + 1, n, W));
     const uint32_t lbyte = lane * kGran;
+    // first byte this lane loads from each 1 KiB row
+    const uint32_t loff = L64 ? 64u * (lane & 15u) + 16u * (lane >> 4) : lbyte;
     // Valid dummy address for the optional seeds (the value is discarded).
     const uint32_t *const seeds_p = seeds ? seeds : g_x8;
 
@@ -1194,7 +1200,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         const uint8_t *src = in ? base + a : (UNI ? base + ua0 : reinterpret_cast<const uint8_t *>(g_x8));
 #pragma unroll
         for (int q = 0; q < kSub; ++q) {
-            r.q[q] = ldg16(src + min(lbyte + (uint32_t) q * kRow, last));
+            r.q[q] = ldg16(src + min(loff + (uint32_t) q * kRow, last));
         }
         if (!UNI) {
             r.inv = load_vec_u32(g_xinv8 + ((uint32_t) kStep - min(vlen, (uint32_t) kStep)));
@@ -1215,7 +1221,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     __builtin_amdgcn_sched_barrier(0);
     // x^(8 * 16 (63 - l)): the lane's fold factor (the register matrix below
     // waits for it), requested right behind the first data.
-    const uint32_t xl = g_x8[kRow - kGran * (lane + 1u)];
+    const uint32_t xl = g_x8[L64 ? 64u * (63u - lane) : kRow - kGran * (lane + 1u)];
     // Uniform batch: one un-shift factor for every chunk.
     const uint32_t inv_u = UNI ? g_xinv8[(uint32_t) kStep - min((uint32_t) uvlen, (uint32_t) kStep)] : 0u;
     __builtin_amdgcn_sched_barrier(0);
@@ -1239,12 +1245,22 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
     // Uniform batch without seeds: the head granule's fix-up (clear the bytes
     // before the content, XOR the initial 0xffffffff in) is the same for every
     // chunk, so its per-lane masks are computed once here.
+    // (L64: the head and the seed, at most bytes 0..18, lie in registers 0
+    // and 1 of lane 0; register k of lane L is granule 4 L + k.)
     uint32_t hk[4] = {~0u, ~0u, ~0u, ~0u}, hs[4] = {0u, 0u, 0u, 0u};
+    uint32_t hk1[4] = {~0u, ~0u, ~0u, ~0u}, hs1[4] = {0u, 0u, 0u, 0u};
     if (UNI && !SEEDS) {
-        const uint4 k = head_fix(make_uint4(~0u, ~0u, ~0u, ~0u), lane, uh, 0u);
-        const uint4 x = head_fix(make_uint4(0u, 0u, 0u, 0u), lane, uh, 0xffffffffu);
+        const uint32_t g0 = L64 ? 4u * lane : lane;
+        const uint4 k = head_fix(make_uint4(~0u, ~0u, ~0u, ~0u), g0, uh, 0u);
+        const uint4 x = head_fix(make_uint4(0u, 0u, 0u, 0u), g0, uh, 0xffffffffu);
         hk[0] = k.x; hk[1] = k.y; hk[2] = k.z; hk[3] = k.w;
         hs[0] = x.x; hs[1] = x.y; hs[2] = x.z; hs[3] = x.w;
+        if (L64) {
+            const uint4 k1 = head_fix(make_uint4(~0u, ~0u, ~0u, ~0u), g0 + 1u, uh, 0u);
+            const uint4 x1 = head_fix(make_uint4(0u, 0u, 0u, 0u), g0 + 1u, uh, 0xffffffffu);
+            hk1[0] = k1.x; hk1[1] = k1.y; hk1[2] = k1.z; hk1[3] = k1.w;
+            hs1[0] = x1.x; hs1[1] = x1.y; hs1[2] = x1.z; hs1[3] = x1.w;
+        }
     }
     __syncthreads();
 
@@ -1262,16 +1278,27 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
             for (int q = 0; q < kSub; ++q) {
                 r.q[q] = cur.q[q];
             }
+            if (L64) {
+                transpose64(r);
+            }
             if (UNI && !SEEDS) {
                 r.q[0] = make_uint4((r.q[0].x & hk[0]) ^ hs[0], (r.q[0].y & hk[1]) ^ hs[1],
                                     (r.q[0].z & hk[2]) ^ hs[2], (r.q[0].w & hk[3]) ^ hs[3]);
+                if (L64) {
+                    r.q[1] = make_uint4((r.q[1].x & hk1[0]) ^ hs1[0], (r.q[1].y & hk1[1]) ^ hs1[1],
+                                        (r.q[1].z & hk1[2]) ^ hs1[2], (r.q[1].w & hk1[3]) ^ hs1[3]);
+                }
+            } else if (L64) {
+                r.q[0] = head_fix(r.q[0], 4u * lane, h, seed);
+                r.q[1] = head_fix(r.q[1], 4u * lane + 1u, h, seed);
             } else {
                 r.q[0] = head_fix(r.q[0], lane, h, seed);
             }
             if (vlen < (uint32_t) kStep) {
 #pragma unroll
                 for (int q = 0; q < kSub; ++q) {
-                    r.q[q] = mask_tail(r.q[q], lbyte + (uint32_t) q * kRow, vlen);
+                    r.q[q] = mask_tail(r.q[q], L64 ? 64u * lane + 16u * (uint32_t) q : lbyte + (uint32_t) q * kRow,
+                                       vlen);
                 }
             }
             if (SMALL_EXP & 2) {
@@ -1284,7 +1311,8 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
                 st = block16(lds, lb_lo, lb_hi, 0u, r.q[0]);
 #pragma unroll
                 for (int q = 1; q < kSub; ++q) {
-                    st = shift_block16(lds, lb_lo, lb_hi, lrep, st, r.q[q]);
+                    st = L64 ? block16(lds, lb_lo, lb_hi, st, r.q[q])
+                             : shift_block16(lds, lb_lo, lb_hi, lrep, st, r.q[q]);
                 }
             }
         }
@@ -2069,8 +2097,13 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
     if (p->small && !cid) {
-        auto sk = p->unsteps ? (dev_seeds ? crc32_small_kernel<true, true> : crc32_small_kernel<true, false>)
-                             : (dev_seeds ? crc32_small_kernel<false, true> : crc32_small_kernel<false, false>);
+        auto sk = p->l64 ? (p->unsteps ? (dev_seeds ? crc32_small_kernel<true, true, true>
+                                                    : crc32_small_kernel<true, false, true>)
+                                       : (dev_seeds ? crc32_small_kernel<false, true, true>
+                                                    : crc32_small_kernel<false, false, true>))
+                         : (p->unsteps ? (dev_seeds ? crc32_small_kernel<true, true> : crc32_small_kernel<true, false>)
+                                       : (dev_seeds ? crc32_small_kernel<false, true>
+                                                    : crc32_small_kernel<false, false>));
         hipLaunchKernelGGL(sk, dim3(p->grid), dim3(kThreads), 0, s,
                            reinterpret_cast<const uint8_t *>(dev_base), p->ustride, p->ua0, p->uvlen, p->uh,
                            p->W, p->n, p->ntiny, st->x8, p->desc, p->tiny, dev_seeds, dev_out, st->xinv8);

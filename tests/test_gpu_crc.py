@@ -139,8 +139,11 @@ def _uniform(n, ln, stride, mis, seed):
     (3000, 3008, 0),      # uniform partial step
     (4, 16, 0),           # smallest chunk that takes the stream path
     (4096, 4112, 5),      # virtual length 4101: two steps, main kernel
+    (4081, 4096, 15),     # 15-byte head: head + seed reach granule 1 (register 1 of lane 0 in L64)
 ])
-def test_small_chunk_uniform_batches(cuda, ln, stride, mis):
+@pytest.mark.parametrize("l64", ["0", "1"])
+def test_small_chunk_uniform_batches(cuda, monkeypatch, ln, stride, mis, l64):
+    monkeypatch.setenv("CIO_GPU_L64", l64)
     buf, offs, lens = _uniform(9000, ln, stride, mis, seed=ln + mis)
     want = po.crc_batch(buf, offs, lens)
     np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), want)
@@ -150,10 +153,12 @@ def test_small_chunk_uniform_batches(cuda, ln, stride, mis):
                                   po.crc_batch(buf, offs, lens, seeds=seeds))
 
 
-def test_small_chunk_mixed_batch_and_kernel_agreement(cuda, monkeypatch):
+@pytest.mark.parametrize("l64", ["0", "1"])
+def test_small_chunk_mixed_batch_and_kernel_agreement(cuda, monkeypatch, l64):
     # every chunk within one 4 KiB wave-step (virtual length <= 4096), with
     # tiny/empty chunks, random misalignment and seeds; the small-chunk kernel
     # and the stream kernel (CIO_GPU_SMALL=0) must agree with the oracle.
+    monkeypatch.setenv("CIO_GPU_L64", l64)
     rng = np.random.default_rng(11)
     n = 30000
     mis = rng.integers(0, 16, n)
@@ -169,7 +174,9 @@ def test_small_chunk_mixed_batch_and_kernel_agreement(cuda, monkeypatch):
     np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, ln, seeds=seeds), want)
 
 
-def test_small_chunk_fewer_chunks_than_waves(cuda):
+@pytest.mark.parametrize("l64", ["0", "1"])
+def test_small_chunk_fewer_chunks_than_waves(cuda, monkeypatch, l64):
+    monkeypatch.setenv("CIO_GPU_L64", l64)
     for n in (1, 2, 63, 4095, 4097):
         buf, offs, lens = _uniform(n, 4096, 4096, 0, seed=n)
         np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
