@@ -398,6 +398,19 @@ __device__ __forceinline__ void load_step64(StepRegs &r, const uint8_t *cbase, u
     }
 }
 
+// The same with each granule clamped to the chunk's last one (general
+// batches: partial last steps, as load_step).
+__device__ __forceinline__ void load_step64c(StepRegs &r, const uint8_t *cbase, uint64_t jj, uint64_t vlen,
+                                             uint32_t lane)
+{
+    const uint64_t b0 = jj * kStep + (uint64_t) (64u * (lane & 15u) + 16u * (lane >> 4));
+    const uint64_t last = (vlen - 1) & ~15ull;
+#pragma unroll
+    for (int q = 0; q < kSub; ++q) {
+        r.q[q] = ldg16(cbase + min(b0 + (uint64_t) q * kRow, last));
+    }
+}
+
 __device__ __forceinline__ void swap16(uint32_t &a, uint32_t &b)
 {
     const auto t = __builtin_amdgcn_permlane16_swap(a, b, false, false);
@@ -465,6 +478,58 @@ __device__ __forceinline__ void slow_compute(const char *lds, uint32_t lb_lo, ui
         s[q] = st;
         e[q] = bs + vb;
     }
+}
+
+// slow_compute for the L64 layout (registers already transposed): the
+// lane's one chain over its granules [64 L + 16 k, +16) of step jj, each
+// clipped to the virtual length, with the head fix-up on granules 0 and 1
+// of lane 0 in the chunk's first step.  A lane with no byte left in the
+// step keeps its state and end.
+__device__ __forceinline__ void slow_compute64(const char *lds, uint32_t lb_lo, uint32_t lb_hi, uint32_t lrep,
+                                               const StepRegs &r, uint64_t jj, uint64_t vlen, uint32_t h,
+                                               uint32_t seed, uint32_t lane, uint32_t &s0, uint64_t &e0)
+{
+    const uint64_t b0 = jj * kStep + 64ull * lane;
+    if (b0 >= vlen) {
+        return;
+    }
+    uint32_t st = step_shift(lds, lrep, s0);
+#pragma unroll
+    for (int k = 0; k < kSub; ++k) {
+        const uint64_t bs = b0 + 16ull * (uint64_t) k;
+        const uint32_t vb = bs >= vlen ? 0u : (uint32_t) min(vlen - bs, (uint64_t) kGran);
+        if (vb == 0) {
+            continue;
+        }
+        uint32_t w[4] = {r.q[k].x, r.q[k].y, r.q[k].z, r.q[k].w};
+        if (jj == 0 && lane == 0 && k < 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int off = 16 * k + 4 * i - (int) h;
+                if (off <= -4) {
+                    w[i] = 0u;
+                } else if (off < 0) {
+                    w[i] = (w[i] & (~0u << (8 * -off))) ^ (seed << (8 * -off));
+                } else if (off == 0) {
+                    w[i] ^= seed;
+                } else if (off < 4) {
+                    w[i] ^= seed >> (8 * off);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if ((uint32_t) (4 * i + 4) <= vb) {
+                st = word_step(lds, lb_lo, lb_hi, st, w[i]);
+            } else if ((uint32_t) (4 * i) < vb) {
+                for (uint32_t t = 4 * i; t < vb; ++t) {
+                    st = byte_step(lds, lb_lo, st, (w[i] >> (8 * (t - 4 * i))) & 0xffu);
+                }
+            }
+        }
+        e0 = bs + vb;
+    }
+    s0 = st;
 }
 
 // First step of a chunk on the fast path: zero the h alignment-head bytes
@@ -703,7 +768,11 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             }
         } else {
         const uint64_t jj = nload > 0 ? lj : (uint64_t) ld.nsteps - 1;
-        load_step(r, lbase + ld.a, jj, ld.vlen, lane);
+        if (L64) {
+            load_step64c(r, lbase + ld.a, jj, ld.vlen, lane);
+        } else {
+            load_step(r, lbase + ld.a, jj, ld.vlen, lane);
+        }
         }
         if (nload > 0) {
             --nload;
@@ -803,12 +872,18 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // step's loads are issued, so their latency overlaps the fold.
         auto crc_step = [&](StepRegs &r) -> bool {
             {
-                if (L64) {
+                if (L64 && (AHEAD || j < full_end)) {
                     // one chain per lane: jump 4032 bytes, then 64 contiguous bytes
                     const uint32_t h0 = step_shift(lds, lrep, s[0]);
                     transpose64(r);
                     if (j == 0) {
-                        r.q[0].x ^= lane == 0 ? seed : 0u;   // h = 0: the seed on content bytes 0..3
+                        if (AHEAD) {
+                            r.q[0].x ^= lane == 0 ? seed : 0u;   // h = 0: the seed on content bytes 0..3
+                        } else {
+                            // head bytes and seed: granules 0 and 1 of lane 0 (4 L + k)
+                            r.q[0] = head_fix(r.q[0], 4u * lane, d.h, seed);
+                            r.q[1] = head_fix(r.q[1], 4u * lane + 1u, d.h, seed);
+                        }
                     }
                     uint32_t st = block16(lds, lb_lo, lb_hi, h0, r.q[0]);
 #pragma unroll
@@ -816,6 +891,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         st = block16(lds, lb_lo, lb_hi, st, r.q[q]);
                     }
                     s[0] = st;
+                    if (!AHEAD) {
+                        e[0] = j * kStep + 64ull * (lane + 1);
+                    }
+                } else if (L64) {
+                    transpose64(r);
+                    slow_compute64(lds, lb_lo, lb_hi, lrep, r, j, d.vlen, d.h, seed, lane, s[0], e[0]);
                 } else if (AHEAD || j < full_end) {
                     // The 4080-byte jump of every sub-chain needs only its
                     // state: its lookups go out before the first use of the
@@ -1732,6 +1813,8 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
 
 namespace cioa {
 
+constexpr bool kL64Default = false;
+
 // Tuning knobs (environment, read at plan creation) and grid geometry.
 void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
 {
@@ -1740,6 +1823,12 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     if (const char *r = getenv("CIO_GPU_PRIO")) {
         const int v = atoi(r);
         p->prio = (v == 0) ? 0 : 1;
+    }
+    // Lane layout of the CRC kernels: one 64-byte chain per lane (L64,
+    // permlane transpose) unless CIO_GPU_L64=0 (the 4-sub-chain layout).
+    p->l64 = kL64Default;
+    if (const char *r = getenv("CIO_GPU_L64")) {
+        p->l64 = atoi(r) != 0;
     }
     p->grid = (uint32_t) st->cus;
     // Test knob: fewer workgroups than CUs (e.g. a wave count that is not a
@@ -1951,9 +2040,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         short_ranges = atoi(r) != 0;
     }
     p->ahead = p->ahead && short_ranges;
-    if (const char *r = getenv("CIO_GPU_L64")) {
-        p->l64 = atoi(r) != 0;
-    }
+
     // All chunks within one wave-step (S = number of non-tiny chunks): the
     // small-chunk kernel (CIO_GPU_SMALL=0 disables).
     p->small = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
@@ -2062,6 +2149,12 @@ static StreamKernel select_kernel(int prio, bool stamps, bool uniform, bool ahea
                         : crc32_stream_kernel<false, 0, true, true, true>;
         }
         return prio ? crc32_stream_kernel<false, 1, true, true> : crc32_stream_kernel<false, 0, true, true>;
+    }
+    if (l64 && !stamps) {
+        // (uniform batches that are not aligned take the general path too: the
+        // uniform L64 instantiation spilled registers)
+        return prio ? crc32_stream_kernel<false, 1, false, false, true>
+                    : crc32_stream_kernel<false, 0, false, false, true>;
     }
     switch ((prio ? 4 : 0) + (stamps ? 2 : 0) + (uniform ? 1 : 0)) {
     case 0: return crc32_stream_kernel<false, 0, false>;

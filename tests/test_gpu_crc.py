@@ -17,6 +17,15 @@ pytestmark = pytest.mark.gpu
 INIT = 0xFFFFFFFF
 
 
+@pytest.fixture(autouse=True, params=["l64", "sub4"])
+def layout(request, monkeypatch):
+    """Every test in this module runs with both lane layouts of the CRC
+    kernels: L64 (one 64-byte chain per lane, permlane transpose) and the
+    4-sub-chain layout (CIO_GPU_L64 = 1 / 0, read at plan creation)."""
+    monkeypatch.setenv("CIO_GPU_L64", "1" if request.param == "l64" else "0")
+    return request.param
+
+
 def to_dev(buf, cuda):
     import torch
     return torch.from_numpy(np.ascontiguousarray(buf)).to(cuda)
