@@ -112,7 +112,8 @@ struct cio_crc32_plan {
     uint32_t unsteps = 0, uh = 0;
     bool small = false;        // every chunk fits one wave-step: crc32_small_kernel
     bool ahead = false;        // uniform, 16-B aligned, whole 4 KiB steps: issue-ahead stream kernel
-    bool l64 = false;          // issue-ahead kernel with one 64-byte chain per lane (CIO_GPU_L64)
+    bool l64 = false;          // stream kernels: one 64-byte chain per lane (CIO_GPU_L64)
+    bool l64_small = false;    // the same layout in the small-chunk kernel
     unsigned long long *stamps = nullptr;   // CIO_GPU_STAMPS=1: diagnostic timestamps
     uint64_t bytes = 0;        // sum of lens
     cioa::ChunkDesc *desc = nullptr;

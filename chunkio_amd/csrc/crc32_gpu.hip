@@ -1813,8 +1813,6 @@ void cio_crc32_plan_destroy(cio_crc32_plan *p)
 
 namespace cioa {
 
-constexpr bool kL64Default = false;
-
 // Tuning knobs (environment, read at plan creation) and grid geometry.
 void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
 {
@@ -1824,11 +1822,15 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
         const int v = atoi(r);
         p->prio = (v == 0) ? 0 : 1;
     }
-    // Lane layout of the CRC kernels: one 64-byte chain per lane (L64,
-    // permlane transpose) unless CIO_GPU_L64=0 (the 4-sub-chain layout).
-    p->l64 = kL64Default;
+    // Lane layout of the CRC kernels (profiles/r03/ab_l64_*.txt): the
+    // stream kernels take one 64-byte chain per lane (L64, permlane
+    // transpose: cfg2 -5 %, cfg3 -1 %, 4 MiB chunks -1 to -2.5 %); the small
+    // kernel keeps the 4-sub-chain layout (L64 there: cfg4k +1 %, 64 Ki x
+    // 4 KiB -3.5 %).  CIO_GPU_L64=1 / 0 forces one layout on both.
+    p->l64 = true;
+    p->l64_small = false;
     if (const char *r = getenv("CIO_GPU_L64")) {
-        p->l64 = atoi(r) != 0;
+        p->l64 = p->l64_small = atoi(r) != 0;
     }
     p->grid = (uint32_t) st->cus;
     // Test knob: fewer workgroups than CUs (e.g. a wave count that is not a
@@ -2190,7 +2192,7 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
         HIP_TRY(hipEventRecord(ev0, s), "hipEventRecord");
     }
     if (p->small && !cid) {
-        auto sk = p->l64 ? (p->unsteps ? (dev_seeds ? crc32_small_kernel<true, true, true>
+        auto sk = p->l64_small ? (p->unsteps ? (dev_seeds ? crc32_small_kernel<true, true, true>
                                                     : crc32_small_kernel<true, false, true>)
                                        : (dev_seeds ? crc32_small_kernel<false, true, true>
                                                     : crc32_small_kernel<false, false, true>))
