@@ -1782,10 +1782,11 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
-    return "chunkio_amd crc32 v8 gfx950 stream(ring1 pre-shift prio-rotate coalesced-nt 4x16B-subchains division-free-start "
-           "slice4-lds32x perm horner-fold direct-whole preshifted-partials wg-lds-fold) small(dpp-reduce bitop3-fold prio-rotate) "
-           "host(nt-staging graduated-groups pread-bounce multi-device) "
-           "sha1(2-schedule-waves 4-block-handover)";
+    return "chunkio_amd crc32 v9 gfx950 stream(l64-lanes permlane-transpose issue-ahead<=64steps pre-shift prio-rotate "
+           "coalesced-nt division-free-start slice4-lds32x perm direct-whole preshifted-partials wg-lds-fold) "
+           "small(4x16B dpp-reduce bitop3-fold prio-rotate) "
+           "host(nt-staging graduated-groups pread-bounce multi-device vpclmul-crc_update small-batch-route) "
+           "sha1(2-schedule-waves 4-block-handover continuation)";
 }
 
 int cio_gpu_init(void)

@@ -5,7 +5,7 @@
 # bench line's kernel paired with that run's own line.  Each GPU step has its
 # own time limit; the script stops at the first failure.
 # Usage (GPU box, repo root): bash tools/r03_check.sh TAG [PHASES]
-#   PHASES: comma list of test,ab,bench,spawn,cross,rsdyn,prof (default: all but rsdyn)
+#   PHASES: comma list of test,ab,bench,spawn,cross,rsdyn,prof,pmc,pmc4k (default: test,ab,bench,spawn,cross,prof)
 set -u
 TAG=${1:-r03}
 OUT=gpurun_out/$TAG
@@ -49,7 +49,9 @@ if has prof; then
         python3 bench.py --config $cfg --steps $k --warmup $w --no-cpu --no-extra > $d.json 2> $d.err
     python3 tools/prof_pair.py $d.json $(find $d -name "run_kernel_trace.csv" | head -1) $kern $iso > $d.pair.json
   done
-  # cfg4k HBM traffic on the final small kernel (separate FETCH / WRITE passes)
-  step pmc_cfg4k 300 bash tools/pmc_configs.sh cfg4k
+fi
+if has pmc; then
+  # HBM traffic of the final kernels (separate FETCH / WRITE passes)
+  step pmc 600 bash tools/pmc_configs.sh ${PMC_CFGS:-cfg2 cfg3 cfg4 cfg4k}
 fi
 echo done
