@@ -62,6 +62,12 @@ ablib:
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(BLD)/ab/crc32_gpu_$(VAR).o $(SRC)/crc32_gpu.hip
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(OUT)/ab/$(VAR).so $(COBJS) $(BLD)/ab/crc32_gpu_$(VAR).o $(BLD)/host_pipeline.o $(BLD)/sha1_gpu.o -lpthread
 
+# Same for the SHA-1 kernel: make ablib_sha1 VAR=name DEFS="-DCIO_SHA1_CHAINS=32"
+ablib_sha1:
+	@mkdir -p $(OUT)/ab $(BLD)/ab
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(BLD)/ab/sha1_gpu_$(VAR).o $(SRC)/sha1_gpu.hip
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(OUT)/ab/$(VAR).so $(COBJS) $(BLD)/crc32_gpu.o $(BLD)/host_pipeline.o $(BLD)/ab/sha1_gpu_$(VAR).o -lpthread
+
 asm: $(SRC)/crc32_gpu.hip
 	@mkdir -p $(BLD)/asm
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(BLD)/asm/crc32_gpu.s $<
@@ -70,4 +76,4 @@ clean:
 	rm -rf $(BLD) $(LIB) $(CTEST)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean ctests ablib
+.PHONY: all oracle asm clean ctests ablib ablib_sha1

@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "crc32_host.h"
@@ -153,21 +154,51 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
     st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
 }
 
-// One workgroup = one round wave + kShaSched schedule waves for the same 64
-// chunks (one chunk per lane), each wave alone on its SIMD.
-//  - Schedule wave s loads blocks j = s, s + kShaSched, ... (kShaAhead of its
-//    own blocks in flight), byte-swaps them, expands the message schedule and
-//    writes K_t + W_t for the 80 rounds to LDS.
+// The same, calling after_row(r) after the 4 rounds of row r (the round
+// wave issues its next block's row reads there, spread over the block).
+template <typename F>
+__device__ __forceinline__ void sha1_block_rounds_spread(Sha1State &st, const uint4 (&rows)[20], F &&after_row)
+{
+    uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        const uint32_t kwv[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * r + u;
+            const uint32_t f = t < 20 ? ch3(b, c, d) : (t < 40 || t >= 60) ? xor3(b, c, d) : maj3(b, c, d);
+            const uint32_t tmp = rotl(a, 5) + f + e + kwv[u];
+            e = d;
+            d = c;
+            c = rotl(b, 30);
+            b = a;
+            a = tmp;
+        }
+        after_row(r);
+    }
+    st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+}
+
+// One workgroup = one round wave + kShaSched schedule waves for the same
+// kShaChains (32) chunks, each wave alone on its SIMD.
+//  - A schedule wave's 64 lanes are 64 / kShaChains block streams of those
+//    chunks (lane = stream * 32 + chunk: lanes 0-31 build block j, lanes
+//    32-63 block j + 1).  Each lane loads its blocks (kShaAhead in flight),
+//    byte-swaps them, expands the message schedule and writes K_t + W_t for
+//    the 80 rounds to LDS.
 //  - The round wave runs only the dependent round chain, 5 VALU per round.
+//    Its lanes 32-63 run the same chains as lanes 0-31 and their results are
+//    dropped: a wave with half its lanes masked off ran the rounds and the
+//    LDS reads ~15% slower (profiles/r03/sha1/ab_sha1_exec_r03j.txt,
+//    ab_sha1_masked_asm_r03j.txt).
 // A lone wave issues one VALU instruction per ~4 cycles
 // (tools/probe/sha1_round_probe.hip: 20.35 cycles per 5-instruction round, in
-// any dependency order), so a chain's floor is ~1630 cycles per block.  One
-// schedule wave needed more than that per block (~250 instructions plus its
-// LDS writes: a build whose round wave did no rounds took 4.5 ms per cfg5
-// batch), so it, not the chain, set the pace; two schedule waves halve it.
-// Blocks are handed over kShaPer (4) at a time through 2 kShaPer LDS slots
-// (160 KiB), one barrier per group (a barrier per block cost ~3 cycles per
-// round).
+// any dependency order), so a chain's floor is ~1630 cycles per block; the
+// round wave alone on register-resident rows ran cfg5 in 4.65 ms.  The
+// round wave reads block j + 1's 20 rows while block j's rounds run, so the
+// reads' latency is hidden; what they still cost (~6% of the chain) is
+// their issue and register-file writes.  Blocks are handed over kShaPer (4)
+// at a time through 2 kShaPer LDS slots, one barrier per group (~0.4%).
 #ifdef CIO_SHA1_GROUP
 constexpr int kShaPer = CIO_SHA1_GROUP;           // blocks handed over per barrier
 #else
@@ -176,14 +207,22 @@ constexpr int kShaPer = 4;
 #ifdef CIO_SHA1_SCHED_WAVES
 constexpr int kShaSched = CIO_SHA1_SCHED_WAVES;   // schedule waves
 #else
-constexpr int kShaSched = 2;
+constexpr int kShaSched = 1;
+#endif
+#ifdef CIO_SHA1_CHAINS
+constexpr int kShaChains = CIO_SHA1_CHAINS;       // chunks per workgroup (64, 32 or 16)
+#else
+constexpr int kShaChains = 32;
 #endif
 constexpr int kShaRowsPerBlock = 20;              // 80 rounds as 20 rows of 4 (ds_read/write_b128)
-constexpr int kShaAhead = 4;                      // own blocks in flight per schedule wave
+constexpr int kShaAhead = 4;                      // own blocks in flight per schedule lane
 constexpr int kShaSlots = 2 * kShaPer;            // one group being read, one being written
 constexpr int kShaThreads = 64 * (1 + kShaSched);
-static_assert(kShaPer % kShaSched == 0, "every schedule wave builds the same number of blocks per group");
-static_assert((kShaAhead * kShaSched) % kShaPer == 0, "a ring turn covers whole groups");
+constexpr int kShaStreams = kShaSched * (64 / kShaChains);   // block streams over the schedule lanes
+static_assert(kShaChains == 64 || kShaChains == 32 || kShaChains == 16, "chunks per workgroup divide a wave");
+static_assert(kShaPer % kShaStreams == 0, "every schedule stream builds the same number of blocks per group");
+static_assert((kShaAhead * kShaStreams) % kShaPer == 0, "a ring turn covers whole groups");
+static_assert(kShaPer % 2 == 0, "the round wave's rows alternate between two register sets");
 
 // kCont = false: one-shot digests (SHA1_Init + SHA1_Update + SHA1_Final per
 // chunk).  kCont = true: SHA1_Update over a per-chunk cio_sha1_state: the
@@ -196,11 +235,11 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests,
             cio_sha1_state *__restrict__ states, uint32_t n)
 {
-    __shared__ uint4 kw[kShaSlots][kShaRowsPerBlock][64];   // [slot][t / 4][lane] = K + W for t..t+3
-    const uint32_t lane = threadIdx.x & 63u;
+    __shared__ uint4 kw[kShaSlots][kShaRowsPerBlock][kShaChains];   // [slot][t / 4][chunk] = K + W for t..t+3
+    const uint32_t lane = threadIdx.x & (kShaChains - 1);   // this thread's chunk in the workgroup
     const bool sched = threadIdx.x >= 64;
-    const uint32_t sw = sched ? (threadIdx.x >> 6) - 1 : 0;   // this schedule wave's block residue
-    const uint32_t i = blockIdx.x * 64 + lane;
+    const uint32_t sw = sched ? (threadIdx.x - 64) / kShaChains : 0;   // a schedule lane's block stream
+    const uint32_t i = blockIdx.x * kShaChains + lane;
     const bool live = i < n;
     const uint32_t ic = live ? i : n - 1;
     const uint8_t *p = base + offs[ic];
@@ -211,19 +250,21 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t vlen = len + num;
     const uint64_t full = vlen / 64;
     const uint64_t nblk = live ? (kCont ? full : full + ((len - full * 64) < 56 ? 1 : 2)) : 0;
-    // The wave's block count: lanes with fewer blocks idle (masked) at the end.
-    uint64_t wmax = nblk;
+    // The workgroup's largest and smallest block counts (every wave holds all
+    // of its chunks): lanes past their last block idle (masked) at the end.
+    uint64_t wmax = nblk, wmin = nblk;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         wmax = max(wmax, (uint64_t) __shfl_xor((unsigned long long) wmax, o));
+        wmin = min(wmin, (uint64_t) __shfl_xor((unsigned long long) wmin, o));
     }
     const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
 
     if (sched) {
         // Aligned content blocks come from a kShaAhead-deep register ring
-        // (this wave's block j + kShaAhead kShaSched is requested when block j
-        // is consumed): the 64 lanes read 64 chunks far apart, and one block
-        // of prefetch did not cover the HBM latency.
+        // (this lane's block j + kShaAhead kShaStreams is requested when block
+        // j is consumed): the lanes read chunks far apart, and one block of
+        // prefetch did not cover the HBM latency.
         // Block j's bytes start at vbase + 64 j (vbase = p for one-shot
         // digests; p - num for a continuation, whose block 0 mixes the
         // pending bytes with the first data bytes and is gathered bytewise:
@@ -232,11 +273,11 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const bool aligned = ((uintptr_t) vbase & 15u) == 0;
         const uint4 *q = reinterpret_cast<const uint4 *>(vbase);
         const uint64_t lo = num > 0 ? 1 : 0;
-        constexpr uint64_t kStride = (uint64_t) kShaAhead * kShaSched;
+        constexpr uint64_t kStride = (uint64_t) kShaAhead * kShaStreams;
         uint4 nx[kShaAhead][4];
 #pragma unroll
         for (int u = 0; u < kShaAhead; ++u) {
-            const uint64_t ub = sw + (uint64_t) u * kShaSched;   // this wave's u-th block
+            const uint64_t ub = sw + (uint64_t) u * kShaStreams;   // this lane's u-th block
             const uint64_t b = ub < full ? ub : (full ? full - 1 : 0);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
@@ -289,24 +330,26 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                     }
                     v[u] = wt + sha1_k(t);
                 }
-                row[r * 64] = make_uint4(v[0], v[1], v[2], v[3]);
+                row[r * kShaChains] = make_uint4(v[0], v[1], v[2], v[3]);
             }
         };
         // Group g = blocks [g kShaPer, (g + 1) kShaPer) is in LDS before
         // barrier g: every schedule wave meets the round wave there after its
-        // last block of the group (ngroups barriers per wave).  Unrolled so
-        // each ring slot is a fixed register set.
+        // last block of the group, plus one final barrier that publishes
+        // nothing (ngroups + 1 per wave, as the round wave's pipeline takes).
+        // Unrolled so each ring slot is a fixed register set.
         for (uint64_t jb = 0; jb < ngroups * kShaPer; jb += kStride) {
 #pragma unroll
             for (int u = 0; u < kShaAhead; ++u) {
-                if (jb + (uint64_t) u * kShaSched < ngroups * kShaPer) {
-                    produce(jb + sw + (uint64_t) u * kShaSched, nx[u]);
-                    if ((u * kShaSched) % kShaPer == kShaPer - kShaSched) {
+                if (jb + (uint64_t) u * kShaStreams < ngroups * kShaPer) {
+                    produce(jb + sw + (uint64_t) u * kShaStreams, nx[u]);
+                    if ((u * kShaStreams) % kShaPer == kShaPer - kShaStreams) {
                         __syncthreads();
                     }
                 }
             }
         }
+        __syncthreads();
         return;
     }
 
@@ -315,44 +358,101 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const cio_sha1_state &s0 = states[i];
         st = {s0.h[0], s0.h[1], s0.h[2], s0.h[3], s0.h[4]};
     }
-    auto load_group = [&](uint64_t g, uint4 (&rows)[kShaPer][kShaRowsPerBlock]) {
+    // Block-level pipeline: block j + 1's 20 rows are requested before block
+    // j's rounds and land while they run.  The barrier that publishes group
+    // g + 1 is taken at the start of group g's last block, once that block's
+    // rows are in registers (after it the schedule waves refill group g's
+    // slots).
+    uint4 ra[kShaRowsPerBlock], rb[kShaRowsPerBlock];
+    auto load_block = [&](uint64_t jb, uint4 (&rows)[kShaRowsPerBlock]) {
+        const uint4 *row = &kw[jb % kShaSlots][0][lane];
 #pragma unroll
-        for (int u = 0; u < kShaPer; ++u) {
-            const uint4 *row = &kw[(g * kShaPer + u) % kShaSlots][0][lane];
-#pragma unroll
-            for (int r = 0; r < kShaRowsPerBlock; ++r) {
-                rows[u][r] = row[r * 64];
-            }
+        for (int r = 0; r < kShaRowsPerBlock; ++r) {
+            rows[r] = row[r * kShaChains];
         }
     };
-    auto run_group = [&](uint64_t g, const uint4 (&rows)[kShaPer][kShaRowsPerBlock]) {
-#pragma unroll
-        for (int u = 0; u < kShaPer; ++u) {
-            // Every lane runs the rounds (the wave issues them anyway) and a
-            // lane past its last block keeps its state: no branch for the
-            // compiler to sink the row reads into, so they stay in order.
-            // (A per-lane branch instead measured 5% slower: the compiler
-            // then spilled rows to AGPRs, sha1_ab_branch.txt.)
+    // kAll: every chunk of the workgroup has block jb.  Otherwise every lane
+    // still runs the rounds (the wave issues them anyway) and a lane past its
+    // last block keeps its state through a select (a per-lane branch measured
+    // 5% slower in round 2: the compiler then spilled rows).
+    auto run_block = [&](auto kAll, uint64_t jb, const uint4 (&rows)[kShaRowsPerBlock]) {
+        if (decltype(kAll)::value) {
+            sha1_block_rounds(st, rows);
+            return;
+        }
+        Sha1State nxs = st;
+        sha1_block_rounds(nxs, rows);
+        const bool take = jb < nblk;
+        st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
+        st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
+    };
+#ifdef CIO_SHA1_SPREAD
+    // Block jb + 1's row reads issued one per 4 rounds of block jb (a burst
+    // of 20 exceeds the 15 reads lgkmcnt can count).
+    auto run_block_spread = [&](auto kAll, uint64_t jb, const uint4 (&rows)[kShaRowsPerBlock],
+                                uint4 (&next)[kShaRowsPerBlock]) {
+        const uint4 *nrow = &kw[(jb + 1) % kShaSlots][0][lane];
+        auto after_row = [&](int r) {
+            next[r] = nrow[r * kShaChains];
+        };
+        if (decltype(kAll)::value) {
+            sha1_block_rounds_spread(st, rows, after_row);
+        } else {
             Sha1State nxs = st;
-            sha1_block_rounds(nxs, rows[u]);
-            const bool take = g * kShaPer + u < nblk;
+            sha1_block_rounds_spread(nxs, rows, after_row);
+            const bool take = jb < nblk;
             st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
             st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
         }
+        // The scheduler's order for this block: one row read, then 20 VALU
+        // (the 4 rounds of a row), 20 times.
+#pragma unroll
+        for (int r = 0; r < kShaRowsPerBlock; ++r) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+            __builtin_amdgcn_sched_group_barrier(0x002, 20, 0);  // VALU
+        }
     };
-    for (uint64_t g = 0; g < ngroups; ++g) {
-        __syncthreads();
-        // All 20 rows of every block of the group are requested up front, so
-        // the LDS latency after the barrier is paid once per group.
-        uint4 rows[kShaPer][kShaRowsPerBlock];
-        load_group(g, rows);
-        // Every row lands before the rounds start: LDS data arriving while the
-        // round chain issues slows the chain more than the wait costs
-        // (profiles/r02/sha1/sha1_ab_wait.txt, sha1_ab_ahead.txt).
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-        run_group(g, rows);
+    auto run_group = [&](auto kAll, uint64_t g) {
+#pragma unroll
+        for (int u = 0; u < kShaPer; ++u) {
+            const uint64_t jb = g * kShaPer + u;
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this block's rows
+            if (u == kShaPer - 1) {
+                __syncthreads();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            run_block_spread(kAll, jb, (u & 1) ? rb : ra, (u & 1) ? ra : rb);
+        }
+    };
+#else
+    auto run_group = [&](auto kAll, uint64_t g) {
+#pragma unroll
+        for (int u = 0; u < kShaPer; ++u) {
+            const uint64_t jb = g * kShaPer + u;
+            // This block's rows (requested a block ago) have landed; waiting
+            // here lets the rounds below run while 20 newer reads are out
+            // (more than lgkmcnt's 4-bit count can wait past).
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+            if (u == kShaPer - 1) {
+                __syncthreads();
+            }
+            load_block(jb + 1, (u & 1) ? ra : rb);   // after the last group: read, not used
+            __builtin_amdgcn_sched_barrier(0);       // the next block's reads go out before the rounds
+            run_block(kAll, jb, (u & 1) ? rb : ra);
+        }
+    };
+#endif
+    __syncthreads();
+    load_block(0, ra);
+    const uint64_t gall = wmin / kShaPer;   // groups every chunk has in full: no selects
+    uint64_t g = 0;
+    for (; g < gall; ++g) {
+        run_group(std::true_type(), g);
     }
-    if (!live) {
+    for (; g < ngroups; ++g) {
+        run_group(std::false_type(), g);
+    }
+    if (!live || threadIdx.x >= kShaChains) {
         return;
     }
     if (kCont) {
@@ -464,7 +564,7 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
     if (n > 0xFFFFFFFFull - 63) {
         return cioa_fail_msg("cio_sha1_batch_dev", "too many chunks for one launch");
     }
-    const dim3 grid((uint32_t) ((n + 63) / 64));
+    const dim3 grid((uint32_t) ((n + kShaChains - 1) / kShaChains));
     const uint8_t *b = reinterpret_cast<const uint8_t *>(dev_base);
     if (dev_states) {
         hipLaunchKernelGGL(sha1_kernel<true>, grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens, nullptr,

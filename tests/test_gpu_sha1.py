@@ -84,7 +84,7 @@ def test_async_device_descriptors(cuda, golden):
 
 
 def test_many_workgroups_ragged_and_misaligned(cuda):
-    """20,011 chunks (313 workgroups of 64 lanes, more than one per CU) with
+    """20,011 chunks (626 workgroups of 32 chunks, more than one per CU) with
     lengths 0..3000 at arbitrary byte offsets: lanes of one wave end at
     different blocks and most take the byte-wise message path."""
     import torch
@@ -98,6 +98,40 @@ def test_many_workgroups_ragged_and_misaligned(cuda):
     dev = torch.from_numpy(host).to(cuda)
     got = cio.sha1_batch_dev(dev, offs, lens)
     for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
+
+
+@pytest.mark.parametrize("update", [False, True])
+def test_select_free_groups(cuda, update):
+    """The round wave runs the groups every chunk of its workgroup has in full
+    without per-lane selects, then the rest with them.  Workgroups (32 chunks)
+    of equal lengths whose block count is a multiple of the 4-block group, one
+    more, three more; one with a single empty chunk (no select-free group); one
+    with a single long chunk among short ones; a partial last workgroup.  Both
+    the one-shot digest and SHA1_Update + SHA1_Final."""
+    import torch
+    rng = np.random.default_rng(24)
+    groups = [
+        [64 * 40 - 9] * 32,                       # 40 blocks with padding: 10 whole groups
+        [64 * 41 - 9] * 32,                       # 41 blocks
+        [64 * 43 - 9] * 32,                       # 43 blocks
+        [0] + [64 * 40] * 31,                     # one empty chunk
+        [5000] + [100] * 31,                      # one long chunk
+        [64 * 12 + 5] * 7,                        # partial workgroup
+    ]
+    lens = np.array([x for g in groups for x in g], np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    total = int(offs[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    dev = torch.from_numpy(host).to(cuda)
+    if update:
+        states = cio.sha1_states_init(len(lens), cuda)
+        cio.sha1_update_batch_dev(dev, _dev_i64(offs, cuda), _dev_i64(lens, cuda), states)
+        got = cio.sha1_final_batch_dev(states)
+    else:
+        got = cio.sha1_batch_dev(dev, offs, lens)
+    for i in range(len(lens)):
         o, ln = int(offs[i]), int(lens[i])
         assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
 
