@@ -154,31 +154,6 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
     st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
 }
 
-// The same, calling after_row(r) after the 4 rounds of row r (the round
-// wave issues its next block's row reads there, spread over the block).
-template <typename F>
-__device__ __forceinline__ void sha1_block_rounds_spread(Sha1State &st, const uint4 (&rows)[20], F &&after_row)
-{
-    uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
-#pragma unroll
-    for (int r = 0; r < 20; ++r) {
-        const uint32_t kwv[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = 4 * r + u;
-            const uint32_t f = t < 20 ? ch3(b, c, d) : (t < 40 || t >= 60) ? xor3(b, c, d) : maj3(b, c, d);
-            const uint32_t tmp = rotl(a, 5) + f + e + kwv[u];
-            e = d;
-            d = c;
-            c = rotl(b, 30);
-            b = a;
-            a = tmp;
-        }
-        after_row(r);
-    }
-    st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
-}
-
 // One workgroup = one round wave + kShaSched schedule waves for the same
 // kShaChains (32) chunks, each wave alone on its SIMD.
 //  - A schedule wave's 64 lanes are 64 / kShaChains block streams of those
@@ -386,45 +361,6 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
         st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
     };
-#ifdef CIO_SHA1_SPREAD
-    // Block jb + 1's row reads issued one per 4 rounds of block jb (a burst
-    // of 20 exceeds the 15 reads lgkmcnt can count).
-    auto run_block_spread = [&](auto kAll, uint64_t jb, const uint4 (&rows)[kShaRowsPerBlock],
-                                uint4 (&next)[kShaRowsPerBlock]) {
-        const uint4 *nrow = &kw[(jb + 1) % kShaSlots][0][lane];
-        auto after_row = [&](int r) {
-            next[r] = nrow[r * kShaChains];
-        };
-        if (decltype(kAll)::value) {
-            sha1_block_rounds_spread(st, rows, after_row);
-        } else {
-            Sha1State nxs = st;
-            sha1_block_rounds_spread(nxs, rows, after_row);
-            const bool take = jb < nblk;
-            st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
-            st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
-        }
-        // The scheduler's order for this block: one row read, then 20 VALU
-        // (the 4 rounds of a row), 20 times.
-#pragma unroll
-        for (int r = 0; r < kShaRowsPerBlock; ++r) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-            __builtin_amdgcn_sched_group_barrier(0x002, 20, 0);  // VALU
-        }
-    };
-    auto run_group = [&](auto kAll, uint64_t g) {
-#pragma unroll
-        for (int u = 0; u < kShaPer; ++u) {
-            const uint64_t jb = g * kShaPer + u;
-            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this block's rows
-            if (u == kShaPer - 1) {
-                __syncthreads();
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            run_block_spread(kAll, jb, (u & 1) ? rb : ra, (u & 1) ? ra : rb);
-        }
-    };
-#else
     auto run_group = [&](auto kAll, uint64_t g) {
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
@@ -441,7 +377,6 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             run_block(kAll, jb, (u & 1) ? rb : ra);
         }
     };
-#endif
     __syncthreads();
     load_block(0, ra);
     const uint64_t gall = wmin / kShaPer;   // groups every chunk has in full: no selects
