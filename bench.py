@@ -475,12 +475,23 @@ def run_sha1(args, rank, world, device, dist):
         bytes(got[i]) == hashlib.sha1(wl.gen_chunk(seed, int(ids[i]) if ids is not None else i,
                                                    int(lens[i])).tobytes()).digest() for i in sample),
              "sample_chunks": sample}
+    # The bound: one wave's issue rate on the dependent round chain
+    # (tools/probe/sha1_round_probe.hip: 20.35 cycles per 5-VALU round at
+    # 2.40 GHz, profiles/r02/sha1/sha1_round_probe.txt) times the longest
+    # chunk's blocks (message + padding).
+    max_blocks = int(((lens.astype(np.uint64) + 8) // 64 + 1).max())
+    floor_s = max_blocks * 80 * 20.35 / 2.40e9
+    floor_gbs = int(lens.sum()) / floor_s / 1e9
     return {"metric": "device-resident SHA-1 GB/s over N×400KB chunks (cfg5)", "value": round(value, 3),
             "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {**desc, "workload": "cfg5: SHA-1 over 1024 x 409600 B per GPU"},
-            "roofline": {"bound": "valu-latency", "achieved": round(value / world, 2),
+            "roofline": {"bound": "valu-issue (round chain)", "achieved": round(value / world, 2),
+                         "issue_floor_GBps": round(floor_gbs, 2),
+                         "frac_of_issue_floor": round(value / world / floor_gbs, 4),
+                         "issue_floor_source": "tools/probe/sha1_round_probe.hip: 20.35 cycles per round "
+                                               "at 2.40 GHz x 80 rounds x the longest chunk's blocks",
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(value / world / HBM_PEAK_GBS, 5),
                          "traffic": load_pmc_traffic("sha1", int(lens.sum())),

@@ -6,6 +6,7 @@
 # own time limit; the script stops at the first failure.
 # Usage (GPU box, repo root): bash tools/r03_check.sh TAG [PHASES]
 #   PHASES: comma list of test,ab,bench,spawn,cross,rsdyn,prof,pmc,pmc4k (default: test,ab,bench,spawn,cross,prof)
+#   env PROF_CFGS=cfg2,sha1 limits the prof phase; PMC_CFGS the pmc phase
 set -u
 TAG=${1:-r03}
 OUT=gpurun_out/$TAG
@@ -44,6 +45,7 @@ if has prof; then
               "cfg3 5 2 crc32_stream_kernel 5" "sha1 10 2 sha1_kernel 0"; do
     set -- $spec
     cfg=$1; k=$2; w=$3; kern=$4; iso=$5
+    [[ ",${PROF_CFGS:-$cfg}," == *",$cfg,"* ]] || continue
     d=$OUT/prof_${cfg}_k$k
     step prof_${cfg}_k$k 300 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
         python3 bench.py --config $cfg --steps $k --warmup $w --no-cpu --no-extra > $d.json 2> $d.err
