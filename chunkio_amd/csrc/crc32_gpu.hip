@@ -1647,27 +1647,23 @@ read_stream_dyn_kernel(const uint8_t *__restrict__ base, uint64_t S, uint64_t Ss
     for (uint64_t g = g0; g < g1; ++g) {
         step(g);
     }
-    uint32_t c = ((blockIdx.x & 7u) * (NC / 8u) + ((threadIdx.x >> 6) % (NC / 8u))) % NC;
-    uint32_t tries = 0;
-    auto claim = [&](uint32_t cc) -> uint32_t {
+    // Counter c = wave mod NC: every counter is shared by waves of every XCD
+    // (so a slow XCD's share flows to the others), and a wave leaves after
+    // its own counter's first failed claim (one extra atomic per wave, no
+    // sequential tries over other counters).  Unit k of counter c covers
+    // pool steps [(k NC + c) U, +U): the counters interleave over the pool.
+    const uint32_t c = wave % NC;
+    auto claim = [&]() -> uint32_t {
         uint32_t u = 0;
         if (lane == 0) {
-            u = __hip_atomic_fetch_add(&ctr[cc * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u = __hip_atomic_fetch_add(&ctr[c * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return __builtin_amdgcn_readfirstlane(u);
     };
-    uint32_t u = claim(c);
-    while (tries < NC) {
-        if (u >= upc) {
-            c = (c + 1u) % NC;
-            ++tries;
-            u = claim(c);
-            continue;
-        }
-        const uint32_t unit = c * upc + u;
-        const uint32_t cur_c = c;
-        (void) cur_c;
-        u = claim(c);    // the next claim in flight while this unit streams
+    uint32_t u = claim();
+    while (u < upc) {
+        const uint32_t unit = u * NC + c;
+        u = claim();    // the next claim in flight while this unit streams
         if (unit < npool) {
             const uint64_t a = Sst + (uint64_t) unit * U;
             const uint64_t b = min(S, a + U);
@@ -2348,8 +2344,8 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
     }
     if (const char *r = getenv("CIO_GPU_RS_DYN")) {
         unsigned pm = 0, U = 4, NC = 64;
-        if (sscanf(r, "%u,%u,%u", &pm, &U, &NC) >= 1 && pm > 0 && pm <= 1000 && U >= 1 && NC >= 8 &&
-            NC <= 1024 && NC % 8 == 0) {
+        if (sscanf(r, "%u,%u,%u", &pm, &U, &NC) >= 1 && pm > 0 && pm <= 1000 && U >= 1 && NC >= 1 &&
+            NC <= 1024) {
             static thread_local uint32_t *ctr = nullptr;
             if (!ctr) {
                 HIP_TRY(hipMalloc(&ctr, 1024 * 32 * sizeof(uint32_t)), "read_stream: hipMalloc");
