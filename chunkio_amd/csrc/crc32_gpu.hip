@@ -892,7 +892,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                     }
                     s[0] = st;
                     if (!AHEAD) {
-                        e[0] = j * kStep + 64ull * (lane + 1);
+                        e[0] = (uint64_t) j * kStep + 64ull * (lane + 1);
                     }
                 } else if (L64) {
                     transpose64(r);
@@ -915,7 +915,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         s[q] = block16(lds, lb_lo, lb_hi, h[q], r.q[q]);
                     }
                     if (!AHEAD) {
-                        const uint64_t e0 = j * kStep + (uint64_t) (lane + 1) * kGran;
+                        const uint64_t e0 = (uint64_t) j * kStep + (uint64_t) (lane + 1) * kGran;
 #pragma unroll
                         for (int q = 0; q < kSub; ++q) {
                             e[q] = e0 + (uint64_t) q * kRow;
@@ -946,7 +946,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         asm volatile("" : "+v"(a));
                         contrib = multmodp(a, L64 ? s[0] : fold_full<UNIFORM>(s));
                     } else {
-                        const uint64_t pend = min(j * kStep, d.vlen);
+                        const uint64_t pend = min((uint64_t) j * kStep, d.vlen);
                         contrib = 0;
 #pragma unroll
                         for (int q = 0; q < kSub; ++q) {
