@@ -132,6 +132,38 @@ def test_more_chunks_than_waves(cuda):
     np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens), po.crc_batch(buf, offs, lens))
 
 
+def test_overlapping_duplicate_and_unordered_chunks(cuda):
+    """Descriptors are independent: chunks may overlap, repeat the same bytes,
+    and come in any address order (a chunk's bytes are only read).  Both the
+    stream kernel (long chunks) and the small kernel (<= 4 KiB), the device
+    and the host batch."""
+    rng = np.random.default_rng(31)
+    buf = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    for lo, hi in ((4, 4097), (4097, 600000)):
+        lens = rng.integers(lo, hi, 300).astype(np.uint64)
+        offs = rng.integers(0, len(buf) - hi - 16, 300).astype(np.uint64)
+        offs[1::7] = offs[0::7][:len(offs[1::7])]            # duplicates of earlier descriptors
+        lens[1::7] = lens[0::7][:len(lens[1::7])]
+        offs[2::7] = offs[1::7][:len(offs[2::7])] + 3        # overlapping, shifted by 3 bytes
+        order = np.argsort(-offs.astype(np.int64))            # descending addresses
+        offs, lens = offs[order], lens[order]
+        seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+        want = po.crc_batch(buf, offs, lens, seeds=seeds)
+        np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds), want, err_msg=f"dev {lo}")
+        np.testing.assert_array_equal(cio.crc32_batch_host_packed(buf, offs, lens, seeds=seeds), want,
+                                      err_msg=f"host {lo}")
+
+
+def test_many_empty_chunks(cuda):
+    """100,000 empty chunks: every CRC is its seed, no data is read."""
+    n = 100000
+    rng = np.random.default_rng(32)
+    seeds = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    offs = rng.integers(0, 64, n).astype(np.uint64)
+    lens = np.zeros(n, np.uint64)
+    np.testing.assert_array_equal(gpu_crc(cuda, np.zeros(128, np.uint8), offs, lens, seeds=seeds), seeds)
+
+
 def _uniform(n, ln, stride, mis, seed):
     """n chunks of ln bytes at mis + i * stride (a uniform batch)."""
     offs = (mis + np.arange(n, dtype=np.uint64) * np.uint64(stride)).astype(np.uint64)
