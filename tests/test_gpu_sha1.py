@@ -102,6 +102,26 @@ def test_many_workgroups_ragged_and_misaligned(cuda):
         assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
 
 
+def test_bit_length_high_word(cuda):
+    """A chunk of 512 MiB + 77 bytes: the 64-bit message bit length in the
+    padding has a non-zero high word (FIPS 180-4 5.1.1), one-shot and through
+    SHA1_Update (two pieces) + SHA1_Final.  One serial chain: ~7 s each."""
+    import torch
+    n = (512 << 20) + 77
+    gen = torch.Generator(device=cuda)
+    gen.manual_seed(0x5A1B)
+    dev = torch.randint(0, 256, (n + 64,), dtype=torch.uint8, device=cuda, generator=gen)
+    host = dev.cpu().numpy()
+    want = hashlib.sha1(host[3:3 + n].tobytes()).digest()
+    got = cio.sha1_batch_dev(dev, np.array([3], np.uint64), np.array([n], np.uint64))
+    assert bytes(got[0]) == want
+    states = cio.sha1_states_init(1, cuda)
+    cut = (300 << 20) + 5
+    cio.sha1_update_batch_dev(dev, _dev_i64([3], cuda), _dev_i64([cut], cuda), states)
+    cio.sha1_update_batch_dev(dev, _dev_i64([3 + cut], cuda), _dev_i64([n - cut], cuda), states)
+    assert bytes(cio.sha1_final_batch_dev(states)[0]) == want
+
+
 @pytest.mark.parametrize("update", [False, True])
 def test_select_free_groups(cuda, update):
     """The round wave runs the groups every chunk of its workgroup has in full
