@@ -476,6 +476,40 @@ def test_host_pipeline_concurrent_callers(cuda):
         assert list(map(int, results[k])) == [po.crc_update(INIT, b) for b in bufs]
 
 
+def test_device_batches_from_concurrent_threads(cuda):
+    """Eight threads each run device batches (their own plans and streams, the
+    small and the stream kernel) at the same time as the others."""
+    import threading
+    import torch
+    rng = np.random.default_rng(13)
+    jobs = []
+    for k in range(8):
+        lens = rng.integers(0, 4097 if k % 2 else 300000, 400).astype(np.uint64)
+        buf, offs = wl.host_batch(0x7000 + k, lens)
+        jobs.append((buf, offs, lens, po.crc_batch(buf, offs, lens)))
+    errors = []
+
+    def run(k):
+        try:
+            buf, offs, lens, want = jobs[k]
+            dev = torch.from_numpy(buf).to(cuda)
+            torch.cuda.synchronize(cuda)      # the upload (current stream) before the batches on s
+            s = torch.cuda.Stream(device=cuda)
+            for _ in range(5):
+                got = cio.crc32_batch_dev(dev, offs, lens, stream=s)
+                if not np.array_equal(got, want):
+                    errors.append(k)
+        except Exception as e:     # reported below
+            errors.append((k, repr(e)))
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+
+
 @pytest.mark.gpu
 def test_host_registered_ranges_direct_dma(cuda, tmp_path):
     """Chunks inside ranges pinned in place (cio_crc32_host_register) are
