@@ -156,6 +156,64 @@ def test_select_free_groups(cuda, update):
         assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
 
 
+def test_block_count_boundaries(cuda):
+    """Block counts 1 .. 97 around multiples of 4 and 16 (the 32-chunk kernel's
+    4-block hand-over groups; the 16-block passes and 3-slot ring of the A/B
+    one-chunk-per-wave kernel, sha1_wave_kernel), cycled so that the chunks of
+    one workgroup end in different groups, aligned and misaligned, 1100
+    chunks (more workgroups than fit at once in the A/B kernel's grid)."""
+    import torch
+    rng = np.random.default_rng(25)
+    nblks = [1, 15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 95, 96, 97]
+    # nblk = full + 1 when the tail is < 56 bytes (a 10-byte tail: one padding block)
+    base_lens = [64 * (b - 1) + 10 for b in nblks] + [64 * 47 + 60]   # the last: 49 blocks (2 padding)
+    lens = np.array([base_lens[(i * 7) % len(base_lens)] for i in range(1100)], np.uint64)
+    for align in (16, 1):
+        offs = wl.packed_offsets(lens, align=align, start=0 if align == 16 else 3)
+        total = int(offs[-1] + lens[-1]) + 64
+        host = rng.integers(0, 256, total, dtype=np.uint8)
+        dev = torch.from_numpy(host).to(cuda)
+        got = cio.sha1_batch_dev(dev, offs, lens)
+        for i in range(len(lens)):
+            o, ln = int(offs[i]), int(lens[i])
+            assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), (align, i, ln)
+
+
+def test_concurrent_streams(cuda):
+    """Batches on four streams from four threads, three launches each: every
+    batch gets its own digests (the A/B one-chunk-per-wave kernel's per-device
+    ring is ordered across streams through an event)."""
+    import threading
+
+    import torch
+    rng = np.random.default_rng(26)
+    jobs = []
+    for t in range(4):
+        lens = rng.integers(0, 40000, 300 + 50 * t).astype(np.uint64)
+        offs = wl.packed_offsets(lens, align=16)
+        host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+        jobs.append((torch.from_numpy(host).to(cuda), offs, lens, host))
+    torch.cuda.synchronize()
+    results = [None] * len(jobs)
+
+    def work(t):
+        dev, offs, lens, _ = jobs[t]
+        s = torch.cuda.Stream(device=cuda)
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                results[t] = cio.sha1_batch_dev(dev, offs, lens, stream=s)
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(len(jobs))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    for (dev, offs, lens, host), got in zip(jobs, results):
+        for i in range(len(lens)):
+            o, ln = int(offs[i]), int(lens[i])
+            assert bytes(got[i]) == hashlib.sha1(host[o:o + ln].tobytes()).digest(), i
+
+
 # ---- continuation: SHA1_Init / SHA1_Update / SHA1_Final per chunk ---------
 # (cio_sha1_update_batch_dev / cio_sha1_final_batch_dev; the reference's
 # cio_sha1_init/update/final, src/cio_sha1.c:26-39, and the pre-Final state
