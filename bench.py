@@ -873,6 +873,17 @@ def visible_gpus():
     return n, how
 
 
+def runtime_gpu_count():
+    """torch.cuda.device_count() in a child process (0 if that fails)."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=600)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else 0
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+        return 0
+
+
 def spawn_ranks(args):
     """`python bench.py --gpus N` with no launcher environment: start N rank
     processes of this script (one per GPU, the layout torch.distributed.run
@@ -882,6 +893,10 @@ def spawn_ranks(args):
     import subprocess
     visible, _ = visible_gpus()
     rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1"
+    if visible < args.gpus and not rehearse:
+        # A sysfs layout this count does not know could under-count: ask the
+        # runtime in a child process (this one stays clean for the ranks).
+        visible = max(visible, runtime_gpu_count())
     if visible < args.gpus and not rehearse:
         print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
         return 2
