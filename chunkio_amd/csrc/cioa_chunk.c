@@ -1339,7 +1339,9 @@ cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext
             }
             ents = e2;
         }
-        ents[n].name = strdup(de->d_name);
+        if (!(ents[n].name = strdup(de->d_name))) {
+            continue;
+        }
         ents[n].ch = NULL;
         ents[n].prepared = 0;
         n++;
