@@ -59,6 +59,24 @@ def parse():
     return p.parse_args()
 
 
+def init_gloo_quiet():
+    """init_process_group("gloo") from the launcher's env.  gloo's C++ side
+    prints "[Gloo] Rank r is connected ..." on fd 1 while the mesh connects;
+    fd 1 goes to stderr meanwhile, so rank 0's stdout holds the JSON line
+    alone."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    return dist
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -77,8 +95,7 @@ def dist_setup(args):
         # RCCL communicator is created at all: the contract's barrier and the
         # two scalar reductions (max-over-ranks, per-GPU gather) run on gloo
         # over CPU tensors, for every N.
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+        dist = init_gloo_quiet()
     if args.gpus != world:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     return rank, world, torch.device("cuda", local), dist

@@ -169,3 +169,25 @@ def test_bench_traffic_scales_to_a_shards_launch():
         got = bench.load_pmc_traffic("cfg4", full // world)
         assert got == round(d["traffic_over_algorithmic"] * (full // world))
     assert bench.load_pmc_traffic("no_such_config", 1) is None
+
+
+def test_gloo_init_keeps_stdout_clean():
+    """Two ranks through bench.init_gloo_quiet: gloo's connection messages
+    land on stderr, so rank 0's stdout is exactly what bench.py prints (the
+    driver reads one JSON line there)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, json; sys.path.insert(0, %r); import bench; d = bench.init_gloo_quiet(); "
+            "print(json.dumps({'rank': d.get_rank()})); d.destroy_process_group()" % root)
+    port = str(29500 + os.getpid() % 1000)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
+    for r, (out, _) in enumerate(outs):
+        assert out.splitlines() == ['{"rank": %d}' % r], out
