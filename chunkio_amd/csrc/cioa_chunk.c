@@ -476,7 +476,10 @@ cioa_ctx *cioa_create(const char *root_path, int flags)
     if (!ctx) {
         return NULL;
     }
-    ctx->root = strdup(root_path);
+    if (!(ctx->root = strdup(root_path))) {
+        free(ctx);
+        return NULL;
+    }
     /* sanitize chunk open flags (src/chunkio.c:103-105) */
     if (!(flags & CIO_OPEN_RW) && !(flags & CIO_OPEN_RD)) {
         flags |= CIO_OPEN_RW;
@@ -607,7 +610,10 @@ cioa_stream *cioa_stream_create(cioa_ctx *ctx, const char *name)
     if (!st) {
         return NULL;
     }
-    st->name = strdup(name);
+    if (!(st->name = strdup(name))) {
+        free(st);
+        return NULL;
+    }
     st->ctx = ctx;
     /* appended, creation order (mk_list_add, cio_stream.c:174): the listing
      * walks streams in this order */
@@ -656,6 +662,12 @@ static cioa_chunk *chunk_new(cioa_ctx *ctx, cioa_stream *st, const char *name, i
     }
     ch->name = strdup(name);
     ch->path = strdup(path);
+    if (!ch->name || !ch->path) {
+        free(ch->name);
+        free(ch->path);
+        free(ch);
+        return NULL;
+    }
     ch->ctx = ctx;
     ch->st = st;
     ch->fd = -1;
