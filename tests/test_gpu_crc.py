@@ -647,3 +647,47 @@ def test_verify_paths_multi_device_and_delete(cuda, tmp_path, data400):
     assert np.array_equal(st3, st1)
     import os
     assert [i for i in range(40) if not os.path.exists(paths[i])] == sorted(bad)
+
+
+@pytest.mark.gpu
+def test_verify_paths_large_files_across_staging_groups(cuda, tmp_path):
+    """Chunk files written here byte by byte (header per cio_file.c:45-60 /
+    cio_file_st.h, CRC from zlib over [22, 24 + meta + content)), not by this
+    library: a 150 MB chunk whose CRC region spans several staging groups of
+    the file-range pipeline (4, 8, 16, 32, 64 MiB), a 70 MB one with
+    metadata, small ones between them, and one flipped byte deep inside the
+    large file.  cio_verify_paths must pass exactly the intact files and
+    return their raw CRC states."""
+    import struct
+    import zlib
+    from chunkio_amd import chunkfile as cf
+    rng = np.random.default_rng(31)
+
+    def chunk_file(path, content, meta=b""):
+        region = struct.pack(">H", len(meta)) + meta + content
+        crc = zlib.crc32(region)
+        hdr = bytes([0xC1, 0x00]) + struct.pack(">I", crc) + bytes(4) + struct.pack(">I", len(content)) + bytes(8)
+        with open(path, "wb") as f:
+            f.write(hdr + region)
+        return crc
+
+    sizes = [150_000_003, 4096, 70_000_000, 1, 3_000_000, 0]
+    metas = [b"", b"m", b"meta-" * 300, b"", b"xy", b""]
+    paths, crcs = [], []
+    for i, (n, m) in enumerate(zip(sizes, metas)):
+        p = str(tmp_path / f"chunk{i}")
+        crcs.append(chunk_file(p, rng.integers(0, 256, n, dtype=np.uint8).tobytes(), m))
+        paths.append(p)
+    st, er, raw = cf.verify_paths(paths)
+    assert list(st) == [cf.CIO_OK] * len(paths), (list(st), list(er))
+    assert [int(r) ^ 0xFFFFFFFF for r in raw] == crcs
+    # one flipped byte 100 MB into the big file's content: only it fails
+    with open(paths[0], "r+b") as f:
+        f.seek(24 + 100_000_000)
+        b = f.read(1)
+        f.seek(24 + 100_000_000)
+        f.write(bytes([b[0] ^ 0x40]))
+    st, er, raw = cf.verify_paths(paths)
+    assert int(st[0]) == cf.CIO_CORRUPTED and int(er[0]) == cf.CIO_ERR_BAD_CHECKSUM
+    assert list(st[1:]) == [cf.CIO_OK] * (len(paths) - 1)
+    assert [int(r) ^ 0xFFFFFFFF for r in raw[1:]] == crcs[1:]
