@@ -155,7 +155,7 @@ def routine():
     return L
 
 
-DIAG = set()   # A/B diagnostics (wrong digests): "nowait", "noglc"
+DIAG = set()   # A/B diagnostics (wrong digests): "nowait", "noload", "noglc", "exec=<mask>"
 
 
 def main():
@@ -163,8 +163,15 @@ def main():
     DIAG.update(a for a in sys.argv[1:])
     L = routine()
     if "nowait" in DIAG:   # timing only: rounds use SGPRs whose loads may not have landed
-        L = [l for l in L if l != "s_waitcnt lgkmcnt(0)"]
-        L.insert(L.index(".Lbar%=:"), "s_waitcnt lgkmcnt(0)")
+        # (the waits before the barrier branch and at the exit stay: no load
+        # may land after the routine, in SGPRs the compiler uses again)
+        keep = {L.index(".Ldone%=:") + 1, len(L) - 2}
+        L = [l for i, l in enumerate(L) if l != "s_waitcnt lgkmcnt(0)" or i in keep]
+        i = L.index(".Ldone%=:")
+        L[i + 1:i + 1] = [] if L[i + 1] == "s_waitcnt lgkmcnt(0)" else ["s_waitcnt lgkmcnt(0)"]
+        L.insert(L.index("s_branch .Lbar%="), "s_waitcnt lgkmcnt(0)")
+    if "noload" in DIAG:   # timing only: no scalar loads or waits at all (the rounds' issue floor)
+        L = [l for l in L if not l.startswith("s_load_") and l != "s_waitcnt lgkmcnt(0)"]
     if "noglc" in DIAG:    # timing only: scalar-cache hits allowed (stale rows possible)
         L = [l.replace(" glc", "") for l in L]
     for d in DIAG:
