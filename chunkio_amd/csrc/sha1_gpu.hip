@@ -504,10 +504,11 @@ __global__ void sha1_final_kernel(const cio_sha1_state *__restrict__ states, uin
 // register file writes) and the round's add takes it as its scalar operand.
 // 1024 chunks = 1024 round waves = one per SIMD of the chip.  Measured
 // (profiles/r03/sha1/ab_sha1_wave*): 4.85-4.89 ms for cfg5 against 4.92-4.94
-// for the kernel above (+1%), with every CU busy instead of 32 -- a whole-
-// chip kernel loses clock (its no-wait floor is 4.82 ms against 4.45 at
-// 2.4 GHz) and, past 1024 chunks, runs its groups one after another where
-// the kernel above fills more CUs.  So the product keeps the kernel above.
+// for the kernel above (+1%), with every CU busy instead of 32: its no-wait
+// floor (4.82 ms) is ~7% above 4.07 cycles per instruction at 2.4 GHz (a
+// whole-chip kernel's clock, most likely; not separated), and past 1024
+// chunks it runs its groups one after another where the kernel above fills
+// more CUs.  So the product keeps the kernel above.
 #ifdef CIO_SHA1_WAVE_KERNEL
 //  - A workgroup is kWvChains round waves (one chunk each) and kWvSched
 //    schedule waves; an LDS request above half the CU keeps it alone on its
