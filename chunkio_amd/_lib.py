@@ -6,6 +6,7 @@ any GPU entry point raises ImportError.
 """
 import ctypes
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # CIO_AMD_LIB: alternate build of the same ABI (A/B measurements only).
@@ -102,6 +103,32 @@ def _bind(lib):
     return lib
 
 
+def _pin_hip_runtime():
+    """Make the library share ONE HIP runtime with torch in this process.
+
+    libchunkio_amd.so needs libamdhip64.so.7 (RUNPATH /opt/rocm).  torch ships
+    its own copy under torch/lib and loads it by path, so if this library is
+    loaded before torch the process ends up with two HIP/HSA runtimes; whichever
+    initialises second sees no device ("hipGetDevice: no ROCm-capable device").
+    Loading torch's copy first (RTLD_GLOBAL, without importing torch) lets the
+    soname match it, and torch's later import reuses the same file.
+    CIOA_HIP_RUNTIME=system keeps the /opt/rocm runtime; a path picks that file.
+    """
+    choice = os.environ.get("CIOA_HIP_RUNTIME", "")
+    if choice == "system" or "torch" in sys.modules:
+        return None                 # torch already loaded: the soname matches its copy
+    path = choice
+    if not path:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+        if spec is None or not spec.origin:
+            return None
+        path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+        if not os.path.exists(path):
+            return None
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
 def lib():
     """Load (once) and return the bound library; raise ImportError if absent."""
     global _lib
@@ -109,6 +136,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is not built: run `make` or __graft_entry__.build()")
+        _pin_hip_runtime()
         _lib = _bind(ctypes.CDLL(LIB_PATH))
     return _lib
 

@@ -121,3 +121,26 @@ def test_sha1_entry_points_reject_null_pointers_without_a_gpu():
     offs = (ctypes.c_uint64 * 1)(0)
     assert lib.cio_sha1_batch_dev(buf, offs, offs, None, 1, None) == -1
     assert b"null pointer" in lib.cio_gpu_last_error()
+
+
+def test_library_shares_torchs_hip_runtime_when_loaded_first():
+    """Loaded before torch, the library must bind torch's libamdhip64 (not a
+    second copy from /opt/rocm): two HIP/HSA runtimes in one process leave the
+    second to initialise with no device (seen on the GPU box as
+    'hipGetDevice: no ROCm-capable device' in a lone test_chunkfile run)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys; sys.path.insert(0, {root!r})
+from chunkio_amd import _lib
+_lib.lib()
+assert "torch" not in sys.modules
+hip = sorted({{l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}})
+import torch
+hip2 = sorted({{l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}})
+print(len(hip), len(hip2), hip2[0].startswith(__import__("os").path.dirname(torch.__file__)))
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["1", "1", "True"], r.stdout

@@ -38,6 +38,11 @@ def route(request):
     lib.cio_crc32_set_cpu_max(old)
 
 
+def _gpu_error():
+    from chunkio_amd import _lib
+    return _lib.lib().cio_gpu_last_error()
+
+
 def hdr_crc_be(path):
     with open(path, "rb") as f:
         return struct.unpack(">I", f.read(6)[2:6])[0]
@@ -155,7 +160,8 @@ def test_down_up_keeps_crc(route, tmp_path, data400):
     c.sync()
     raw = c.crc_cur
     assert c.down() == cf.CIO_OK
-    assert c.up() == cf.CIO_OK
+    rc = c.up()
+    assert rc == cf.CIO_OK, (rc, c.error, _gpu_error())
     assert c.crc_cur == raw and c.data_size == len(data400)
     assert struct.unpack(">I", c.hash())[0] == 0x103CFA67
     c.write(b"more")                                             # append after re-verify
@@ -618,3 +624,34 @@ def test_scan_verify_failure_registers_down(tmp_path):
         ctx.close()
     finally:
         lib.cio_crc32_set_cpu_max(old)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["lib_then_torch", "torch_then_lib"])
+def test_gpu_route_with_torch_in_either_load_order(order, cuda):
+    """The GPU verify route of up() and torch's own device work both succeed
+    whichever of the library and torch is loaded and initialised first (one
+    HIP runtime per process; chunkio_amd/_lib.py _pin_hip_runtime)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    first, second = ("from chunkio_amd import _lib, chunkfile as cf", "import torch")
+    if order == "torch_then_lib":
+        first, second = second, first
+    code = f"""
+import os, sys, tempfile; sys.path.insert(0, {root!r})
+{first}
+{second}
+assert torch.cuda.is_available()
+lib = _lib.lib(); lib.cio_crc32_set_cpu_max(0)
+data = bytes(range(256)) * 1601
+c, rc = cf.ChunkFile.open(os.path.join(tempfile.mkdtemp(), "s", "x"))
+assert c.write(data) == 0 and c.sync() == 0 and c.down() == 0
+rc = c.up()
+assert rc == 0, (rc, lib.cio_gpu_last_error())
+t = torch.arange(1000, device="cuda:0").sum().item()
+print("ok", t)
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-2:] == ["ok", "499500"], r.stdout
