@@ -93,14 +93,31 @@ struct HostGroup {
 };
 
 // Persistent host copy workers (the box's CPU share per GPU is 16 threads).
-// copy() cuts a group's byte range into 1 MiB pieces that the workers and
-// the caller claim through one atomic counter, so a slow or descheduled
-// thread delays the group by one piece, not by a 1/16 slice.  The caller
-// first runs `before` (the group's plan build), overlapping it with the
-// workers' copying.
+// copy() cuts a group's byte range into pieces that the workers and the
+// caller claim through one atomic counter, so a slow or descheduled thread
+// delays the group by one piece, not by a 1/16 slice.  Pieces are 1 MiB, or
+// smaller for small groups so every thread gets about two (a call's first
+// 4 MiB group in 1 MiB pieces kept 12 of the 16 threads idle while the DMA
+// engine waited for it).  The caller first runs `before` (the group's plan
+// build), overlapping it with the workers' copying.
 class CopyPool {
 public:
-    static constexpr uint64_t kPiece = 1ull << 20;
+    static constexpr uint64_t kPieceMax = 1ull << 20;
+    static constexpr uint64_t kPieceMin = 64ull << 10;
+
+    uint64_t piece_bytes(uint64_t bytes) const
+    {
+        static const uint64_t fixed = [] {
+            const char *r = getenv("CIO_GPU_COPY_PIECE_KB");   // A/B knob: a fixed piece size
+            const long v = r ? atol(r) : 0;
+            return v >= 4 && v <= 65536 ? (uint64_t) v << 10 : 0;
+        }();
+        if (fixed) {
+            return fixed;
+        }
+        const uint64_t per = bytes / (2 * (workers_.size() + 1));
+        return std::min(kPieceMax, std::max(kPieceMin, (per + kPieceMin - 1) & ~(kPieceMin - 1)));
+    }
 
     CopyPool()
     {
@@ -125,7 +142,8 @@ public:
     template <typename F>
     bool copy(uint8_t *dst, const HostGroup &g, F before)
     {
-        const uint64_t npieces = (g.bytes + kPiece - 1) / kPiece;
+        const uint64_t piece = piece_bytes(g.bytes);
+        const uint64_t npieces = (g.bytes + piece - 1) / piece;
         if (npieces <= 1 || workers_.empty()) {
             before();
             const bool ok = range(dst, g, 0, g.bytes);
@@ -137,6 +155,7 @@ public:
             dst_ = dst;
             g_ = &g;
             npieces_ = npieces;
+            piece_ = piece;
             next_.store(0, std::memory_order_relaxed);
             pending_ = workers_.size();
             failed_ = false;
@@ -144,7 +163,7 @@ public:
         }
         cv_.notify_all();
         before();
-        const bool ok = drain(dst, g, npieces);
+        const bool ok = drain(dst, g, npieces, piece);
         cioa_stage_fence();
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [this] { return pending_ == 0; });
@@ -152,7 +171,7 @@ public:
     }
 
 private:
-    bool drain(uint8_t *dst, const HostGroup &g, uint64_t npieces)
+    bool drain(uint8_t *dst, const HostGroup &g, uint64_t npieces, uint64_t piece)
     {
         bool ok = true;
         for (;;) {
@@ -160,7 +179,7 @@ private:
             if (p >= npieces) {
                 return ok;
             }
-            ok &= range(dst, g, p * kPiece, std::min<uint64_t>(g.bytes, (p + 1) * kPiece));
+            ok &= range(dst, g, p * piece, std::min<uint64_t>(g.bytes, (p + 1) * piece));
         }
     }
     static constexpr uint64_t kBounce = 256u << 10;
@@ -216,7 +235,7 @@ private:
         for (;;) {
             uint8_t *dst;
             const HostGroup *g;
-            uint64_t npieces;
+            uint64_t npieces, piece;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
@@ -227,8 +246,9 @@ private:
                 dst = dst_;
                 g = g_;
                 npieces = npieces_;
+                piece = piece_;
             }
-            const bool ok = drain(dst, *g, npieces);
+            const bool ok = drain(dst, *g, npieces, piece);
             cioa_stage_fence();
             std::lock_guard<std::mutex> lk(mu_);
             failed_ = failed_ || !ok;
@@ -246,6 +266,7 @@ private:
     uint8_t *dst_ = nullptr;
     const HostGroup *g_ = nullptr;
     uint64_t npieces_ = 0;
+    uint64_t piece_ = kPieceMax;
     std::atomic<uint64_t> next_{0};
     size_t pending_ = 0;
 };
