@@ -202,6 +202,15 @@ static_assert(kShaPer % kShaStreams == 0, "every schedule stream builds the same
 static_assert((kShaAhead * kShaStreams) % kShaPer == 0, "a ring turn covers whole groups");
 static_assert(kShaPer % 2 == 0, "the round wave's rows alternate between two register sets");
 
+#ifdef CIO_SHA1_CLOCK_DIAG
+// Diagnostic builds only: per workgroup, the round wave's shader-clock and
+// 100 MHz counters at the start and the end of its block loop (read back by
+// cio_sha1_diag_clock; tools/sha1_clock.py turns them into the clock the
+// kernel ran at and cycles per round).
+constexpr int kClkMax = 8192;
+__device__ unsigned long long g_sha1_clk[kClkMax][4];
+#endif
+
 // kCont = false: one-shot digests (SHA1_Init + SHA1_Update + SHA1_Final per
 // chunk).  kCont = true: SHA1_Update over a per-chunk cio_sha1_state: the
 // virtual message is the state's pending bytes || the chunk's bytes; its
@@ -381,6 +390,10 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         }
     };
     __syncthreads();
+#ifdef CIO_SHA1_CLOCK_DIAG
+    const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     load_block(0, ra);
     const uint64_t gall = wmin / kShaPer;   // groups every chunk has in full: no selects
     uint64_t g = 0;
@@ -390,6 +403,18 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     for (; g < ngroups; ++g) {
         run_group(std::false_type(), g);
     }
+#ifdef CIO_SHA1_CLOCK_DIAG
+    {
+        const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0 && blockIdx.x < kClkMax) {
+            g_sha1_clk[blockIdx.x][0] = clk0;
+            g_sha1_clk[blockIdx.x][1] = clk1;
+            g_sha1_clk[blockIdx.x][2] = rt0;
+            g_sha1_clk[blockIdx.x][3] = rt1;
+        }
+    }
+#endif
     if (!live || threadIdx.x >= kShaChains) {
         return;
     }
@@ -833,6 +858,19 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
 }
 
 }  // namespace
+
+#ifdef CIO_SHA1_CLOCK_DIAG
+// Diagnostic builds only: copy the first nwg workgroups' clock records
+// (4 x u64 each: shader clock start/end, 100 MHz start/end) to host memory.
+extern "C" int cio_sha1_diag_clock(unsigned long long *out, int nwg)
+{
+    if (nwg < 0 || nwg > kClkMax) {
+        return CIO_ERROR;
+    }
+    const hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sha1_clk), (size_t) nwg * 4 * sizeof(unsigned long long));
+    return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_diag_clock", hipGetErrorString(e));
+}
+#endif
 
 extern "C" void cio_sha1_state_init(cio_sha1_state *states, size_t n)
 {
