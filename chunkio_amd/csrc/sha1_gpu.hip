@@ -377,6 +377,15 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
             const uint64_t jb = g * kShaPer + u;
+#ifndef CIO_SHA1_NO_ANCHOR
+            // The rounds are pure arithmetic, so the instruction selector may
+            // move a block's rounds past the next block's reads (it did in the
+            // select-free groups: blocks 3 and 0 then waited on reads issued
+            // just before them).  The previous block's chaining value passes
+            // through an empty volatile asm with a memory clobber here, so
+            // those rounds end before the reads below are issued.
+            asm volatile("" : "+v"(st.h0), "+v"(st.h1), "+v"(st.h2), "+v"(st.h3), "+v"(st.h4) : : "memory");
+#endif
             // This block's rows (requested a block ago) have landed; waiting
             // here lets the rounds below run while 20 newer reads are out
             // (more than lgkmcnt's 4-bit count can wait past).
