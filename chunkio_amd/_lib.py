@@ -47,6 +47,7 @@ EXPORTS = (
 )
 
 _lib = None
+_hip_runtime = None
 
 c_u64_p = ctypes.POINTER(ctypes.c_uint64)
 c_u32_p = ctypes.POINTER(ctypes.c_uint32)
@@ -136,7 +137,8 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is not built: run `make` or __graft_entry__.build()")
-        _pin_hip_runtime()
+        global _hip_runtime
+        _hip_runtime = _pin_hip_runtime()   # kept referenced for the process's lifetime
         _lib = _bind(ctypes.CDLL(LIB_PATH))
     return _lib
 
