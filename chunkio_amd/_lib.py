@@ -132,12 +132,11 @@ def _pin_hip_runtime():
 
 def lib():
     """Load (once) and return the bound library; raise ImportError if absent."""
-    global _lib
+    global _lib, _hip_runtime
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is not built: run `make` or __graft_entry__.build()")
-        global _hip_runtime
         _hip_runtime = _pin_hip_runtime()   # kept referenced for the process's lifetime
         _lib = _bind(ctypes.CDLL(LIB_PATH))
     return _lib
