@@ -144,3 +144,22 @@ print(len(hip), len(hip2), hip2[0].startswith(__import__("os").path.dirname(torc
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["1", "1", "True"], r.stdout
+
+
+def test_hip_runtime_override_system():
+    """CIOA_HIP_RUNTIME=system keeps the library on /opt/rocm's libamdhip64
+    (one runtime as long as torch is not loaded into the same process)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys; sys.path.insert(0, {root!r})
+from chunkio_amd import _lib
+_lib.lib()
+hip = sorted({{l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}})
+print(len(hip), hip[0].startswith("/opt/rocm"), _lib._hip_runtime is None)
+"""
+    env = dict(os.environ, CIOA_HIP_RUNTIME="system")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["1", "True", "True"], r.stdout
