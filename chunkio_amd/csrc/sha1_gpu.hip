@@ -19,6 +19,7 @@
 #include <type_traits>
 #include <vector>
 #include <mutex>
+#include <atomic>
 #include <algorithm>
 #include <stdlib.h>
 
@@ -188,19 +189,40 @@ constexpr int kShaSched = CIO_SHA1_SCHED_WAVES;   // schedule waves
 constexpr int kShaSched = 1;
 #endif
 #ifdef CIO_SHA1_CHAINS
-constexpr int kShaChains = CIO_SHA1_CHAINS;       // chunks per workgroup (64, 32 or 16)
+constexpr int kShaChains = CIO_SHA1_CHAINS;       // chunks per workgroup (64, 32, 16 or 8)
 #else
 constexpr int kShaChains = 32;
 #endif
 constexpr int kShaRowsPerBlock = 20;              // 80 rounds as 20 rows of 4 (ds_read/write_b128)
 constexpr int kShaAhead = 4;                      // own blocks in flight per schedule lane
-constexpr int kShaSlots = 2 * kShaPer;            // one group being read, one being written
 constexpr int kShaThreads = 64 * (1 + kShaSched);
 constexpr int kShaStreams = kShaSched * (64 / kShaChains);   // block streams over the schedule lanes
-static_assert(kShaChains == 64 || kShaChains == 32 || kShaChains == 16, "chunks per workgroup divide a wave");
+static_assert(kShaChains == 64 || kShaChains == 32 || kShaChains == 16 || kShaChains == 8, "chunks per workgroup divide a wave");
 static_assert(kShaPer % kShaStreams == 0, "every schedule stream builds the same number of blocks per group");
 static_assert((kShaAhead * kShaStreams) % kShaPer == 0, "a ring turn covers whole groups");
 static_assert(kShaPer % 2 == 0, "the round wave's rows alternate between two register sets");
+
+// Workgroup geometry as a template argument: C chunks per workgroup, P blocks
+// handed over per barrier.  Fewer chunks per workgroup means fewer distinct
+// row addresses per round-wave read (the lanes repeat the C chains) and
+// measured faster while the grid still fits the chip (1024 x 400 KB:
+// 8 chunks/WG with 8 blocks per barrier 4.813 ms, 16/8 4.822, 16/4 4.831,
+// 32/4 4.862; profiles/r03/sha1/ab_sha1_chains_r03zu.txt), but a round wave
+// then does 64/C times the work per chain, so larger batches keep 32.
+template <int C, int P>
+struct ShaGeom {
+    static constexpr int kChains = C;
+    static constexpr int kPer = P;
+    static constexpr int kSlots = 2 * P;   // one group being read, one being written
+    static constexpr int kStreams = kShaSched * (64 / C);
+    static_assert(C == 64 || C == 32 || C == 16 || C == 8, "chunks per workgroup divide a wave");
+    static_assert(P % kStreams == 0, "every schedule stream builds the same number of blocks per group");
+    static_assert((kShaAhead * kStreams) % P == 0, "a ring turn covers whole groups");
+    static_assert(P % 2 == 0, "the round wave's rows alternate between two register sets");
+};
+using ShaGeomWide = ShaGeom<kShaChains, kShaPer>;   // the default (CIO_SHA1_CHAINS / GROUP for A/B)
+using ShaGeom16 = ShaGeom<16, 8>;
+using ShaGeom8 = ShaGeom<8, 8>;
 
 #ifdef CIO_SHA1_CLOCK_DIAG
 // Diagnostic builds only: per workgroup, the round wave's shader-clock and
@@ -216,12 +238,16 @@ __device__ unsigned long long g_sha1_clk[kClkMax][4];
 // virtual message is the state's pending bytes || the chunk's bytes; its
 // whole blocks are hashed into the state's chaining value and the rest
 // becomes the new pending block (no padding: sha1_final_kernel pads).
-template <bool kCont>
+template <bool kCont, class G>
 __global__ void __launch_bounds__(kShaThreads)
 sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests,
             cio_sha1_state *__restrict__ states, uint32_t n)
 {
+    constexpr int kShaChains = G::kChains;
+    constexpr int kShaPer = G::kPer;
+    constexpr int kShaSlots = G::kSlots;
+    constexpr int kShaStreams = G::kStreams;
     __shared__ uint4 kw[kShaSlots][kShaRowsPerBlock][kShaChains];   // [slot][t / 4][chunk] = K + W for t..t+3
     const uint32_t lane = threadIdx.x & (kShaChains - 1);   // this thread's chunk in the workgroup
     const bool sched = threadIdx.x >= 64;
@@ -842,6 +868,40 @@ int sha1_wave_launch(const uint8_t *b, const uint64_t *dev_offs, const uint64_t 
 }
 #endif  // CIO_SHA1_WAVE_KERNEL
 
+// Chunks per workgroup for a batch of n: the fewest (8, then 16) whose grid
+// still fits one workgroup per CU, else the default geometry.
+// CIO_SHA1_CHUNKS_PER_WG=8|16|32 forces one (tests run every geometry).
+int sha1_chunks_per_wg(size_t n)
+{
+    static const int forced = [] {
+        const char *r = getenv("CIO_SHA1_CHUNKS_PER_WG");
+        const int v = r ? atoi(r) : 0;
+        return (v == 8 || v == 16 || v == 32) ? v : 0;
+    }();
+    if (forced) {
+        return forced == 32 ? kShaChains : forced;
+    }
+    static std::atomic<int> cus_by_dev[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        return kShaChains;
+    }
+    int cus = cus_by_dev[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+            return kShaChains;
+        }
+        cus_by_dev[dev].store(cus, std::memory_order_relaxed);
+    }
+    if (n <= (size_t) 8 * (size_t) cus) {
+        return 8;
+    }
+    if (n <= (size_t) 16 * (size_t) cus) {
+        return 16;
+    }
+    return kShaChains;
+}
+
 int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens, uint8_t *dev_digests,
                 cio_sha1_state *dev_states, size_t n, hipStream_t s)
 {
@@ -853,14 +913,25 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
         return sha1_wave_launch(reinterpret_cast<const uint8_t *>(dev_base), dev_offs, dev_lens, dev_digests, n, s);
     }
 #endif
-    const dim3 grid((uint32_t) ((n + kShaChains - 1) / kShaChains));
     const uint8_t *b = reinterpret_cast<const uint8_t *>(dev_base);
-    if (dev_states) {
-        hipLaunchKernelGGL(sha1_kernel<true>, grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens, nullptr,
-                           dev_states, (uint32_t) n);
+    auto launch = [&](auto geom) {
+        using G = decltype(geom);
+        const dim3 grid((uint32_t) ((n + G::kChains - 1) / G::kChains));
+        if (dev_states) {
+            hipLaunchKernelGGL((sha1_kernel<true, G>), grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens,
+                               nullptr, dev_states, (uint32_t) n);
+        } else {
+            hipLaunchKernelGGL((sha1_kernel<false, G>), grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens,
+                               dev_digests, nullptr, (uint32_t) n);
+        }
+    };
+    const int per_wg = sha1_chunks_per_wg(n);
+    if (per_wg == 8) {
+        launch(ShaGeom8());
+    } else if (per_wg == 16) {
+        launch(ShaGeom16());
     } else {
-        hipLaunchKernelGGL(sha1_kernel<false>, grid, dim3(kShaThreads), 0, s, b, dev_offs, dev_lens, dev_digests,
-                           nullptr, (uint32_t) n);
+        launch(ShaGeomWide());
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev: launch", hipGetErrorString(e));
