@@ -392,6 +392,13 @@ def run_crc(args, rank, world, device, dist):
         want = np.asarray([zlib.crc32(host0[int(o):int(o + n)]) ^ 0xFFFFFFFF for o, n in zip(offs, lens)],
                           dtype=np.uint32)
         check["zlib_match"] = bool(np.array_equal(want, gpu0))
+    if args.config == "cfg3" and world == 1:
+        # every one of the 65,536 CRCs against the reference crc32.c's digest
+        import hashlib
+        with open(os.path.join(ROOT, "tests", "golden", "crc32_vectors.json")) as f:
+            g = json.load(f)["cfg3"]
+        check["golden_sha256_match_all_chunks"] = hashlib.sha256(gpu0.astype("<u4").tobytes()).hexdigest() == \
+            g["sha256_of_raw_le"]
     if args.config in ("cfg3", "cfg4"):
         # Full-size batches: 8 chunks spread over the batch (first, last and
         # evenly between), device bytes copied back and CRC'd with zlib.
@@ -492,6 +499,12 @@ def run_sha1(args, rank, world, device, dist):
         bytes(got[i]) == hashlib.sha1(wl.gen_chunk(seed, int(ids[i]) if ids is not None else i,
                                                    int(lens[i])).tobytes()).digest() for i in sample),
              "sample_chunks": sample}
+    if world == 1:
+        # all 1,024 digests against hashlib's (tests/golden/make_golden.py)
+        with open(os.path.join(ROOT, "tests", "golden", "crc32_vectors.json")) as f:
+            g = json.load(f)["sha1"]
+        check["golden_sha256_match_all_digests"] = hashlib.sha256(got.tobytes()).hexdigest() == \
+            g["cfg5_sha256_of_digests"]
     # The bound: one wave's issue rate on the dependent round chain
     # (tools/probe/sha1_round_probe.hip: 20.35 cycles per 5-VALU round at
     # 2.40 GHz, profiles/r02/sha1/sha1_round_probe.txt) times the longest

@@ -42,6 +42,20 @@ def _cfg4_raw(i):
     return ref_raw(INIT, wl.gen_chunk(wl.CFG4_SEED, i, wl.CFG4_LEN).tobytes())
 
 
+_L3 = None
+
+
+def _cfg3_raw(i):
+    global _L3
+    if _L3 is None:
+        _L3 = wl.cfg3_lens()
+    return ref_raw(INIT, wl.gen_chunk(wl.CFG3_SEED, i, int(_L3[i])).tobytes())
+
+
+def _cfg5_digest(i):
+    return hashlib.sha1(wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes()).digest()
+
+
 def main():
     if pyoracle.ref() is None:
         sys.exit("oracle/_ref/libcrc32_ref.so missing: run `make -C oracle` with /root/reference present")
@@ -88,15 +102,19 @@ def main():
     c2 = [ref_raw(INIT, wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes()) for i in range(wl.CFG2_N)]
     out["cfg2"] = {"seed": wl.CFG2_SEED, "n": wl.CFG2_N, "len": wl.CFG2_LEN, "first32": c2[:32],
                    "sha256_of_raw_le": hashlib.sha256(np.asarray(c2, np.uint32).tobytes()).hexdigest()}
-    # Config 3: geometry digest + raw CRCs of 48 spread chunks.
+    # Config 3: geometry digest, raw CRCs of 48 spread chunks, and a digest of
+    # all 65,536 raw CRCs (39.7 GB through the reference crc32.c and zlib, 6
+    # processes), so the full batch is pinned whole, not by samples.
     l3 = wl.cfg3_lens()
     idx3 = [int(x) for x in np.linspace(0, wl.CFG3_N - 1, 48).astype(int)]
+    with multiprocessing.Pool(6) as pool:
+        c3 = pool.map(_cfg3_raw, range(wl.CFG3_N), chunksize=256)
     out["cfg3"] = {"seed": wl.CFG3_SEED, "n": wl.CFG3_N, "total_bytes": int(l3.sum()),
                    "min_len": int(l3.min()), "max_len": int(l3.max()),
                    "lens_sha256": hashlib.sha256(l3.astype("<u8").tobytes()).hexdigest(),
                    "sample_idx": idx3,
-                   "sample_raw": [ref_raw(INIT, wl.gen_chunk(wl.CFG3_SEED, i, int(l3[i])).tobytes())
-                                  for i in idx3]}
+                   "sample_raw": [c3[i] for i in idx3],
+                   "sha256_of_raw_le": hashlib.sha256(np.asarray(c3, np.uint32).tobytes()).hexdigest()}
     # Config 4: raw CRCs of 8 chunks (one per GPU shard at G=8), and a digest of
     # all 8192 (34.4 GB through the reference crc32.c and zlib, 6 processes),
     # so the sharded full-size job can be checked whole.
@@ -107,13 +125,17 @@ def main():
                    "sample_raw": c4[:8],
                    "sha256_of_raw_le": hashlib.sha256(np.asarray(c4, np.uint32).tobytes()).hexdigest()}
     # SHA-1 (config 5): hashlib (OpenSSL) -- the reference's <sha1/sha1.h> is not vendored.
+    # All 1,024 cfg2-batch digests are pinned by the SHA-256 of their concatenation.
+    with multiprocessing.Pool(6) as pool:
+        c5 = pool.map(_cfg5_digest, range(wl.CFG2_N), chunksize=32)
     out["sha1"] = {"oracle": "hashlib.sha1 (OpenSSL); FIPS 180-4 KATs",
                    "kats": [{"hex": b"abc".hex(), "digest": hashlib.sha1(b"abc").hexdigest()},
                             {"hex": "", "digest": hashlib.sha1(b"").hexdigest()},
                             {"hex": b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq".hex(),
                              "digest": "84983e441c3bd26ebaae4aa1f95129e5e54670f1"}],
-                   "cfg2_first8": [hashlib.sha1(wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes()).hexdigest()
-                                   for i in range(8)],
+                   "cfg2_first8": [d.hex() for d in c5[:8]],
+                   "cfg5_n": wl.CFG2_N,
+                   "cfg5_sha256_of_digests": hashlib.sha256(b"".join(c5)).hexdigest(),
                    "400kb": hashlib.sha1(D400).hexdigest()}
     with open(os.path.join(HERE, "crc32_vectors.json"), "w") as f:
         json.dump(out, f, indent=1)

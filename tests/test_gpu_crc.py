@@ -368,6 +368,8 @@ def test_cfg3_mixed_sizes_full(cuda, golden):
     cio.fill_synthetic(dev, offs, lens, g["seed"])
     got = cio.crc32_batch_dev(dev, offs, lens)
     assert [int(got[i]) for i in g["sample_idx"]] == g["sample_raw"]
+    # every one of the 65,536 CRCs, against the reference crc32.c (make_golden.py)
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_of_raw_le"]
     split_combine_check(cuda, dev, offs, lens, got)
 
 

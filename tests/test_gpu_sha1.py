@@ -38,14 +38,17 @@ def test_padding_boundaries(cuda):
             assert bytes(d) == hashlib.sha1(c).digest(), len(c)
 
 
-def test_cfg5_sample(cuda, golden, data400):
+def test_cfg5_full_batch(cuda, golden, data400):
+    """All 1,024 cfg5 digests, pinned by the SHA-256 of their concatenation
+    (hashlib, tests/golden/make_golden.py)."""
     import torch
-    lens = wl.cfg2_lens(64)
+    lens = wl.cfg2_lens()
     offs = wl.packed_offsets(lens)
     dev = torch.empty(wl.batch_bytes(offs, lens), dtype=torch.uint8, device=cuda)
     cio.fill_synthetic(dev, offs, lens, wl.CFG2_SEED)
     got = cio.sha1_batch_dev(dev, offs, lens)
     assert [bytes(d).hex() for d in got[:8]] == golden["sha1"]["cfg2_first8"]
+    assert hashlib.sha256(got.tobytes()).hexdigest() == golden["sha1"]["cfg5_sha256_of_digests"]
     got400 = run(cuda, [data400])
     assert bytes(got400[0]).hex() == golden["sha1"]["400kb"]
 
@@ -61,6 +64,7 @@ def test_async_device_descriptors(cuda, golden):
     cio.fill_synthetic(dev, offs, lens, wl.CFG2_SEED)
     want = cio.sha1_batch_dev(dev, offs, lens)
     assert [bytes(d).hex() for d in want[:8]] == golden["sha1"]["cfg2_first8"]
+    assert hashlib.sha256(want.tobytes()).hexdigest() == golden["sha1"]["cfg5_sha256_of_digests"]
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(cuda)
     d_lens = torch.from_numpy(lens.astype(np.int64)).to(cuda)
     out = torch.zeros(len(lens) * 20, dtype=torch.uint8, device=cuda)
@@ -68,6 +72,7 @@ def test_async_device_descriptors(cuda, golden):
         cio.sha1_batch_dev_async(dev, d_offs, d_lens, out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().reshape(-1, 20), want)
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == golden["sha1"]["cfg5_sha256_of_digests"]
 
     rng = np.random.default_rng(22)
     rl = rng.integers(0, 20000, 200).astype(np.uint64)
@@ -302,6 +307,7 @@ def test_continuation_appends_cfg5_shape(cuda, golden):
                                   _dev_i64(np.full(n, step), cuda), states)
     got = cio.sha1_final_batch_dev(states)
     assert [bytes(d).hex() for d in got[:8]] == golden["sha1"]["cfg2_first8"]
+    assert hashlib.sha256(got.tobytes()).hexdigest() == golden["sha1"]["cfg5_sha256_of_digests"]
     assert np.array_equal(got, cio.sha1_batch_dev(dev, offs, lens))
     tail = torch.arange(7, dtype=torch.uint8, device=cuda) + 1
     cio.sha1_update_batch_dev(tail, _dev_i64(np.zeros(n), cuda), _dev_i64(np.full(n, 7), cuda), states)

@@ -123,3 +123,25 @@ def test_multithreaded_batch_timer_matches_single_thread():
     f(buf.ctypes.data, offs.ctypes.data_as(u64p), lens.ctypes.data_as(u64p), len(lens), 2, 4,
       out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     np.testing.assert_array_equal(out, po.crc_batch(buf, offs, lens))
+
+
+def test_cfg5_full_digest_fixture(golden):
+    """The cfg5 fixture (SHA-256 over all 1,024 digests) recomputed with
+    hashlib from the generator: the GPU tests compare against this value."""
+    import hashlib
+    d = b"".join(hashlib.sha1(wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes()).digest()
+                 for i in range(wl.CFG2_N))
+    assert hashlib.sha256(d).hexdigest() == golden["sha1"]["cfg5_sha256_of_digests"]
+    assert [d[20 * i:20 * i + 20].hex() for i in range(8)] == golden["sha1"]["cfg2_first8"]
+
+
+def test_cfg3_fixture_samples_and_digest_shape(golden):
+    """cfg3's pinned samples recomputed with zlib (a second oracle beside the
+    reference crc32.c that made them); the 65,536-CRC digest itself is checked
+    on the GPU (test_cfg3_mixed_sizes_full), 39.7 GB being too much for the CPU suite."""
+    import zlib
+    g = golden["cfg3"]
+    l3 = wl.cfg3_lens()
+    for i, raw in list(zip(g["sample_idx"], g["sample_raw"]))[::8]:
+        assert zlib.crc32(wl.gen_chunk(g["seed"], i, int(l3[i])).tobytes()) ^ 0xFFFFFFFF == raw
+    assert len(g["sha256_of_raw_le"]) == 64
