@@ -59,17 +59,26 @@ def parse():
     return p.parse_args()
 
 
+def pg_timeout_s():
+    """Bound on every gloo rendezvous, barrier and scalar reduction: a rank that
+    dies leaves the others blocked for at most this long (gloo's default is 30
+    minutes).  The longest legitimate wait between ranks is one stage's skew
+    (seconds)."""
+    return float(os.environ.get("CIO_BENCH_PG_TIMEOUT_S", "300"))
+
+
 def init_gloo_quiet():
-    """init_process_group("gloo") from the launcher's env.  gloo's C++ side
-    prints "[Gloo] Rank r is connected ..." on fd 1 while the mesh connects;
-    fd 1 goes to stderr meanwhile, so rank 0's stdout holds the JSON line
-    alone."""
+    """init_process_group("gloo") from the launcher's env, with a bounded
+    timeout.  gloo's C++ side prints "[Gloo] Rank r is connected ..." on fd 1
+    while the mesh connects; fd 1 goes to stderr meanwhile, so rank 0's stdout
+    holds the JSON line alone."""
+    import datetime
     import torch.distributed as dist
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=pg_timeout_s()))
         dist.barrier()
     finally:
         os.dup2(saved, 1)
@@ -81,6 +90,31 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Test hook (tests/test_distributed.py): CIO_BENCH_FAIL_RANK=r makes rank r
+    # exit 1 before the rendezvous (CIO_BENCH_FAIL_AT=init), after it while
+    # the others wait in a barrier as they would in the timed region
+    # (=barrier, the default), or hang there (=hang).  The launcher must end
+    # the job promptly in every case, not wait for gloo's timeout.
+    fail_rank = os.environ.get("CIO_BENCH_FAIL_RANK")
+    fail_at = os.environ.get("CIO_BENCH_FAIL_AT", "barrier")
+    failing = fail_rank is not None and int(fail_rank) == rank
+    if failing and fail_at == "init":
+        os._exit(1)
+    dist = None
+    if world > 1:
+        # The data path has no collective (chunks shard round-robin), so no
+        # RCCL communicator is created at all: the contract's barrier and the
+        # two scalar reductions (max-over-ranks, per-GPU gather) run on gloo
+        # over CPU tensors, for every N.  Joined before any GPU work, so a
+        # rank that cannot start fails the job at once.
+        dist = init_gloo_quiet()
+    if fail_rank is not None:
+        if failing and fail_at == "hang":
+            while True:
+                time.sleep(60)
+        if failing:
+            os._exit(1)
+        barrier(dist)
     import torch
     # CIO_BENCH_REHEARSE=1: rehearse the N>1 path on a box with fewer GPUs
     # than ranks (ranks share devices round-robin, gloo for the barrier and
@@ -89,13 +123,6 @@ def dist_setup(args):
     if rehearse:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        # The data path has no collective (chunks shard round-robin), so no
-        # RCCL communicator is created at all: the contract's barrier and the
-        # two scalar reductions (max-over-ranks, per-GPU gather) run on gloo
-        # over CPU tensors, for every N.
-        dist = init_gloo_quiet()
     if args.gpus != world:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     return rank, world, torch.device("cuda", local), dist
@@ -930,15 +957,53 @@ def spawn_ranks(args):
     if visible < args.gpus and not rehearse:
         print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
         return 2
+    import signal
     env = dict(os.environ, WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     procs = []
-    for r in range(args.gpus):
-        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+
+    def stop_all(grace_s=10.0):
+        """SIGTERM every live rank, then SIGKILL what is left after grace_s."""
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.terminate()
+        deadline = time.monotonic() + grace_s
+        for p in live:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    def on_signal(signum, _frame):
+        stop_all()
+        sys.exit(128 + signum)
+
+    old_handlers = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for r in range(args.gpus):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+            print(f"bench.py: rank {r} pid {procs[-1].pid}", file=sys.stderr, flush=True)
+        # Poll every rank (not in order): the first non-zero exit ends the job,
+        # so a rank that dies at init or mid-run cannot leave its siblings
+        # blocked in a barrier until the gloo timeout.
+        while True:
+            rcs = [p.poll() for p in procs]
+            bad = [(r, rc) for r, rc in enumerate(rcs) if rc is not None and rc != 0]
+            if bad:
+                r, rc = bad[0]
+                print(f"bench.py: rank {r} exited with status {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop_all()
+                return rc if rc > 0 else 128 - rc
+            if all(rc == 0 for rc in rcs):
+                return 0
+            time.sleep(0.1)
+    finally:
+        stop_all()
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
 
 
 def other_configs(args, rank, world, device, dist):

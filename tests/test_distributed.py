@@ -191,3 +191,109 @@ def test_gloo_init_keeps_stdout_clean():
     assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
     for r, (out, _) in enumerate(outs):
         assert out.splitlines() == ['{"rank": %d}' % r], out
+
+
+def _spawn_bench(extra_env, gpus=2):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CIO_BENCH_REHEARSE="1", **extra_env)
+    return subprocess.Popen([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus),
+                             "--steps", "1", "--warmup", "0"], env=env,
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+
+def _rank_pids(stderr):
+    import re
+    return [int(m) for m in re.findall(r"bench\.py: rank \d+ pid (\d+)", stderr)]
+
+
+def _gone(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return True
+    # a zombie not yet reaped by init still answers kill(0); check its state
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] == "Z"
+    except OSError:
+        return True
+
+
+@pytest.mark.parametrize("fail_at", ["barrier", "init"])
+def test_bench_spawn_fails_fast_when_a_rank_dies(fail_at):
+    """`bench.py --gpus 2` with rank 1 forced to exit 1 (after the gloo
+    rendezvous, with rank 0 waiting in a barrier; or before it, with rank 0
+    waiting in the rendezvous): the launcher sees the failure, stops rank 0
+    and returns non-zero within seconds -- not after gloo's timeout -- and
+    leaves no rank process behind."""
+    import time
+    t0 = time.monotonic()
+    p = _spawn_bench({"CIO_BENCH_FAIL_RANK": "1", "CIO_BENCH_FAIL_AT": fail_at})
+    out, err = p.communicate(timeout=120)
+    took = time.monotonic() - t0
+    assert p.returncode not in (0, None), err[-2000:]
+    assert took < 60, took
+    assert out == ""
+    pids = _rank_pids(err)
+    assert len(pids) == 2, err[-2000:]
+    assert "rank 1 exited with status 1" in err or "exited with status" in err, err[-2000:]
+    time.sleep(0.5)
+    assert all(_gone(pid) for pid in pids), pids
+
+
+def test_bench_spawn_forwards_sigterm_to_ranks():
+    """A hung rank (rank 1 never reaches the barrier): SIGTERM to the launcher
+    (a driver's time limit) stops every rank before the launcher exits."""
+    import signal
+    import time
+    p = _spawn_bench({"CIO_BENCH_FAIL_RANK": "1", "CIO_BENCH_FAIL_AT": "hang",
+                      "CIO_BENCH_PG_TIMEOUT_S": "600"})
+    # wait until both ranks are up (their pids are printed as they start)
+    import selectors
+    sel = selectors.DefaultSelector()
+    sel.register(p.stderr, selectors.EVENT_READ)
+    buf = ""
+    t0 = time.monotonic()
+    while len(_rank_pids(buf)) < 2 and time.monotonic() - t0 < 60:
+        if sel.select(timeout=1):
+            line = p.stderr.readline()
+            if not line:
+                break
+            buf += line
+    pids = _rank_pids(buf)
+    assert len(pids) == 2, buf
+    time.sleep(3)                        # ranks importing torch / in the rendezvous
+    p.send_signal(signal.SIGTERM)
+    p.communicate(timeout=60)
+    assert p.returncode == 128 + signal.SIGTERM
+    time.sleep(0.5)
+    assert all(_gone(pid) for pid in pids), pids
+
+
+def test_bench_pg_timeout_bounds_a_barrier_without_the_launcher():
+    """Ranks started by another launcher (torch.distributed.run): a barrier on a
+    dead peer ends with an error within the bounded gloo timeout, not 30 min."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import bench, os; d = bench.init_gloo_quiet(); "
+            "r = d.get_rank()\n"
+            "if r == 1: os._exit(1)\n"
+            "d.barrier()" % root)
+    port = str(_free_port())
+    procs = []
+    t0 = time.monotonic()
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, CIO_BENCH_PG_TIMEOUT_S="10")
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        p.communicate(timeout=120)
+    assert procs[1].returncode == 1
+    assert procs[0].returncode != 0
+    assert time.monotonic() - t0 < 60
