@@ -552,321 +552,6 @@ __global__ void sha1_final_kernel(const cio_sha1_state *__restrict__ states, uin
     }
 }
 
-// ---------------------------------------------------------------- one chunk per round wave
-//
-// A/B build only (make ablib_sha1 DEFS=-DCIO_SHA1_WAVE_KERNEL): not the
-// product path.  sha1_wave_kernel (one-shot digests) asks whether the round
-// wave's row reads can leave the chain.  The kernel above is bound by its
-// round wave's instruction issue: 400 VALU per block for the rounds plus 20
-// ds_read_b128 that bring the block's K + W rows into the 32 chains' lanes.
-// Here a round wave runs ONE chunk on all its lanes, so K_t + W_t is
-// wave-uniform: it arrives in SGPRs by scalar loads (6 per block, no vector
-// register file writes) and the round's add takes it as its scalar operand.
-// 1024 chunks = 1024 round waves = one per SIMD of the chip.  Measured
-// (profiles/r03/sha1/ab_sha1_wave*): 4.85-4.89 ms for cfg5 against 4.92-4.94
-// for the kernel above (+1%), with every CU busy instead of 32: its no-wait
-// floor (4.82 ms) is ~7% above 4.07 cycles per instruction at 2.4 GHz (a
-// whole-chip kernel's clock, most likely; not separated), and past 1024
-// chunks it runs its groups one after another where the kernel above fills
-// more CUs.  So the product keeps the kernel above.
-#ifdef CIO_SHA1_WAVE_KERNEL
-//  - A workgroup is kWvChains round waves (one chunk each) and kWvSched
-//    schedule waves; an LDS request above half the CU keeps it alone on its
-//    CU, so every round wave has a SIMD.  Schedule wave s builds the passes p
-//    with p % kWvSched == s, so the SIMD time the schedule takes (~5% of one
-//    SIMD's issue) is spread over the four round waves instead of slowing
-//    one of them (the chunks of a workgroup meet at every pass barrier).
-//  - A schedule wave's lanes are kWvChains chunks x kWvBlocks block streams.
-//    A pass is kWvBlocks consecutive blocks of every chunk: a schedule wave
-//    writes a pass's K + W rows (320 B per block) to the workgroup's ring in
-//    global memory (kWvBufs passes per chunk, consecutive) and they are
-//    published at a workgroup barrier, two passes ahead of the round waves.
-//    The rows stay in the XCD's L2 (~61 KiB per workgroup); the round waves'
-//    scalar loads bypass the scalar cache (glc), which would otherwise return
-//    a previous pass's rows from the same ring slot.
-//  - Barrier b (b = 0, 1, ...) publishes pass b + 1 (and pass 0 at b = 0):
-//    between barriers b and b + 1 the round waves hash pass b and may
-//    prefetch from pass b + 1, while the schedule wave writes pass b + 2 into
-//    the slot of pass b - 1, which every round wave finished before barrier b.
-//  - Persistent: grid = min(groups, CUs); a workgroup walks its groups of
-//    kWvChains chunks, so the ring needs one slot set per resident workgroup.
-#ifdef CIO_SHA1_WAVE_INC
-#include CIO_SHA1_WAVE_INC   // A/B builds of the generated routine
-#else
-#include "sha1_wave_rounds.inc"
-#endif
-constexpr int kWvChains = 4;                     // round waves = chunks per group
-constexpr int kWvBlocks = 16;                    // blocks per chunk per pass
-constexpr int kWvBufs = 3;                       // passes in the ring
-#ifdef CIO_SHA1_WAVE_SCHED
-constexpr int kWvSched = CIO_SHA1_WAVE_SCHED;    // schedule waves (A/B)
-#else
-constexpr int kWvSched = 4;                      // schedule waves: one per SIMD, pass p by wave p % 4
-#endif
-constexpr int kWvThreads = 64 * (kWvChains + kWvSched);
-constexpr int kWvWords = 80;                     // K + W words per block
-constexpr size_t kWvChainWords = CIOA_SHA1_WAVE_CHAIN_STRIDE / 4;   // a chunk's kWvBufs slots + padding
-constexpr size_t kWvSlotWords = CIOA_SHA1_WAVE_SLOT_BYTES / 4;      // a pass's rows of one chunk
-constexpr size_t kWvRingWords = kWvChains * kWvChainWords;          // per workgroup
-static_assert(kWvSlotWords == (size_t) kWvBlocks * 80, "the routine's slot is one pass of the chunk");
-constexpr uint32_t kWvLds = 96u << 10;           // > half of the CU's 160 KiB: one workgroup per CU
-static_assert(kWvChains * kWvBlocks == 64, "one schedule wave: a lane per (chunk, block stream)");
-
-// The round wave's loop (every pass of its chunk: scalar loads of the K + W
-// rows, 5 VALU per round, the pass barriers) is one generated inline-asm
-// routine: sha1_wave_rounds.inc, from tools/gen_sha1_wave_asm.py.  It owns
-// the SGPRs it clobbers from each scalar load to its wait (with the loads in
-// separate asm statements the compiler copied an in-flight SGPR tuple before
-// its wait).
-
-// A wave-uniform value the compiler must keep in a VGPR (the round chain runs
-// on the vector ALU: v_alignbit / v_bitop3 / v_add3 have no scalar forms).
-__device__ __forceinline__ uint32_t vreg(uint32_t x)
-{
-    uint32_t r;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
-    return r;
-}
-
-__global__ void __launch_bounds__(kWvThreads)
-sha1_wave_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-                 const uint64_t *__restrict__ lens, uint8_t *__restrict__ digests, uint32_t *__restrict__ ring_all,
-                 uint32_t n)
-{
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t *ring = ring_all + (size_t) blockIdx.x * kWvRingWords;
-    const uint32_t ngroups = (n + kWvChains - 1) / kWvChains;
-
-    for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-        // Block counts of the group's chunks (uniform loads) and the group's pass count.
-        uint64_t nb[kWvChains];
-        uint64_t wmax = 0;
-#pragma unroll
-        for (int k = 0; k < kWvChains; ++k) {
-            const uint32_t ik = grp * kWvChains + k;
-            const uint64_t lk = ik < n ? lens[ik] : 0;
-            nb[k] = ik < n ? lk / 64 + ((lk % 64) < 56 ? 1 : 2) : 0;
-            wmax = max(wmax, nb[k]);
-        }
-        const uint64_t npass = (wmax + kWvBlocks - 1) / kWvBlocks;
-
-        if (wv >= kWvChains) {
-            // ---- schedule wave sidx: the passes p with p % kWvSched == sidx;
-            //      lane = chunk k * 16 + block stream sw
-            const uint32_t sidx = wv - kWvChains;
-            const uint32_t k = lane / kWvBlocks, sw = lane % kWvBlocks;
-            const uint32_t ik = grp * kWvChains + k;
-            const bool live = ik < n;
-            const uint32_t ic = live ? ik : n - 1;
-            const uint8_t *p = base + offs[ic];
-            const uint64_t len = lens[ic];
-            const uint64_t full = len / 64;
-            const uint64_t nblk = live ? full + ((len - full * 64) < 56 ? 1 : 2) : 0;
-            const bool aligned = ((uintptr_t) p & 15u) == 0;
-            const uint4 *q = reinterpret_cast<const uint4 *>(p);
-            // this lane's next aligned content block (the lane's block of the
-            // wave's next pass), loaded one turn of kWvSched passes ahead
-            uint4 nx[4];
-            {
-                const uint64_t bj = (uint64_t) sidx * kWvBlocks + sw;
-                const uint64_t bl = bj < full ? bj : (full ? full - 1 : 0);
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    nx[v] = (aligned && full > 0) ? q[bl * 4 + v] : make_uint4(0, 0, 0, 0);
-                }
-            }
-            // Block j = pass * 16 + sw into ring slot pass % kWvBufs.
-            auto produce = [&](uint64_t pass) {
-                const uint64_t j = pass * kWvBlocks + sw;
-                if (j >= nblk) {
-                    return;
-                }
-                uint32_t w[16];
-                if (aligned && j < full) {
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        w[4 * v + 0] = bswap32(nx[v].x); w[4 * v + 1] = bswap32(nx[v].y);
-                        w[4 * v + 2] = bswap32(nx[v].z); w[4 * v + 3] = bswap32(nx[v].w);
-                    }
-                    const uint64_t nj = j + (uint64_t) kWvSched * kWvBlocks;
-                    const uint64_t pf = nj < full ? nj : full - 1;   // clamped refill
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        nx[v] = q[pf * 4 + v];
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                } else {
-                    message_block(p, len, full, j, w);
-                }
-                uint4 *row = reinterpret_cast<uint4 *>(ring + k * kWvChainWords + (pass % kWvBufs) * kWvSlotWords +
-                                                       (size_t) sw * kWvWords);
-#pragma unroll
-                for (int r4 = 0; r4 < kWvWords / 4; ++r4) {
-                    uint32_t v[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int t = 4 * r4 + u;
-                        uint32_t wt;
-                        if (t < 16) {
-                            wt = w[t];
-                        } else {
-                            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
-                            w[t & 15] = wt;
-                        }
-                        v[u] = wt + sha1_k(t);
-                    }
-                    row[r4] = make_uint4(v[0], v[1], v[2], v[3]);
-                }
-            };
-            // Barriers 0 .. npass: passes 0 and 1 are written before barrier
-            // 0, pass b + 1 before barrier b.  Rows reach L2 (vector stores
-            // write through) before the barrier that publishes them.
-            for (uint64_t b = 0; b <= npass; ++b) {
-                if (b == 0) {
-                    if (sidx == 0) {
-                        produce(0);
-                    }
-                    if (sidx == 1 % kWvSched) {
-                        produce(1);
-                    }
-                } else if (b + 1 < npass && (b + 1) % kWvSched == sidx) {
-                    produce(b + 1);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-            }
-        } else {
-            // ---- round wave wv: chunk grp * kWvChains + wv, all 64 lanes
-            const uint32_t ik = grp * kWvChains + wv;
-            uint64_t mynb = 0;
-#pragma unroll
-            for (int k = 0; k < kWvChains; ++k) {
-                mynb = (uint32_t) k == wv ? nb[k] : mynb;
-            }
-            const uint64_t rows = (uint64_t) (uintptr_t) (ring + (size_t) wv * kWvChainWords);
-            uint32_t h0 = vreg(0x67452301u), h1 = vreg(0xEFCDAB89u), h2 = vreg(0x98BADCFEu);
-            uint32_t h3 = vreg(0x10325476u), h4 = vreg(0xC3D2E1F0u);
-            uint32_t x0, x1, x2, x3, x4, t, r;
-            // barrier 0, then one barrier per pass (inside the routine)
-            asm volatile(CIOA_SHA1_WAVE_ROUNDS_ASM
-                         : [h0] "+v"(h0), [h1] "+v"(h1), [h2] "+v"(h2), [h3] "+v"(h3), [h4] "+v"(h4),
-                           [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3), [x4] "=&v"(x4),
-                           [t] "=&v"(t), [r] "=&v"(r)
-                         : [blo] "s"(__builtin_amdgcn_readfirstlane((uint32_t) rows)),
-                           [bhi] "s"(__builtin_amdgcn_readfirstlane((uint32_t) (rows >> 32))),
-                           [npass] "s"(__builtin_amdgcn_readfirstlane((uint32_t) npass)),
-                           [nblo] "s"(__builtin_amdgcn_readfirstlane((uint32_t) mynb)),
-                           [nbhi] "s"(__builtin_amdgcn_readfirstlane((uint32_t) (mynb >> 32)))
-                         : CIOA_SHA1_WAVE_ROUNDS_CLOBBERS);
-            if (ik < n && lane == 0) {
-                uint8_t *out = digests + (uint64_t) ik * 20;
-                const uint32_t h[5] = {h0, h1, h2, h3, h4};
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    out[4 * k + 0] = (uint8_t) (h[k] >> 24);
-                    out[4 * k + 1] = (uint8_t) (h[k] >> 16);
-                    out[4 * k + 2] = (uint8_t) (h[k] >> 8);
-                    out[4 * k + 3] = (uint8_t) h[k];
-                }
-            }
-        }
-        // the next group reuses the ring: every wave is past its last read
-        __syncthreads();
-    }
-}
-#endif  // CIO_SHA1_WAVE_KERNEL
-
-}  // namespace
-
-namespace {
-
-#ifdef CIO_SHA1_WAVE_KERNEL
-// The one-shot kernel's K + W ring (kWvRingWords per resident workgroup), per
-// device, grown on demand; and the device's CU count (the persistent grid).
-// Launches on different streams would share the ring, so each launch waits
-// for the previous one (`last`, recorded after it) before it starts: SHA-1
-// batches on one device run one after another (each fills the GPU's CUs).
-// Inside a stream capture the ordering is left to the captured graph.
-struct WaveRing {
-    std::mutex mu;
-    uint32_t *ring = nullptr;
-    size_t wgs = 0;
-    int cus = 0;
-    hipEvent_t last = nullptr;
-};
-WaveRing g_wave_ring[64];
-
-// CIO_SHA1_WAVE=0 selects the 32-chunk kernel for one-shot digests too.
-bool use_wave_kernel()
-{
-    static const bool v = [] {
-        const char *r = getenv("CIO_SHA1_WAVE");
-        return !(r && r[0] == '0');
-    }();
-    return v;
-}
-
-int sha1_wave_launch(const uint8_t *b, const uint64_t *dev_offs, const uint64_t *dev_lens, uint8_t *dev_digests,
-                     size_t n, hipStream_t s)
-{
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess || dev < 0 || dev >= 64) {
-        return cioa_fail_msg("cio_sha1_batch_dev: device", e != hipSuccess ? hipGetErrorString(e) : "ordinal");
-    }
-    WaveRing &wr = g_wave_ring[dev];
-    const size_t groups = (n + kWvChains - 1) / kWvChains;
-    uint32_t *ring;
-    size_t grid;
-    {
-        std::lock_guard<std::mutex> lk(wr.mu);
-        if (wr.cus == 0) {
-            int cus = 0;
-            e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e != hipSuccess || cus <= 0) {
-                return cioa_fail_msg("cio_sha1_batch_dev: CU count", hipGetErrorString(e));
-            }
-            wr.cus = cus;
-        }
-        grid = std::min(groups, (size_t) wr.cus);
-        if (wr.wgs < grid) {
-            // A launch still queued on another stream may use the old ring:
-            // the device is drained before it is replaced.
-            if (wr.ring) {
-                (void) hipDeviceSynchronize();
-                (void) hipFree(wr.ring);
-                wr.ring = nullptr;
-                wr.wgs = 0;
-            }
-            const size_t want = (size_t) wr.cus;   // the largest grid this device launches
-            e = hipMalloc(&wr.ring, want * kWvRingWords * sizeof(uint32_t));
-            if (e != hipSuccess) {
-                return cioa_fail_msg("cio_sha1_batch_dev: ring", hipGetErrorString(e));
-            }
-            wr.wgs = want;
-        }
-        ring = wr.ring;
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        (void) hipStreamIsCapturing(s, &cap);
-        const bool order = cap == hipStreamCaptureStatusNone;
-        if (order && !wr.last && (e = hipEventCreateWithFlags(&wr.last, hipEventDisableTiming)) != hipSuccess) {
-            return cioa_fail_msg("cio_sha1_batch_dev: event", hipGetErrorString(e));
-        }
-        if (order && (e = hipStreamWaitEvent(s, wr.last, 0)) != hipSuccess) {
-            return cioa_fail_msg("cio_sha1_batch_dev: ring order", hipGetErrorString(e));
-        }
-        // kWvLds of dynamic LDS (unused) keeps one workgroup per CU
-        hipLaunchKernelGGL(sha1_wave_kernel, dim3((uint32_t) grid), dim3(kWvThreads), kWvLds, s, b, dev_offs,
-                           dev_lens, dev_digests, ring, (uint32_t) n);
-        e = hipGetLastError();
-        if (e == hipSuccess && order) {
-            e = hipEventRecord(wr.last, s);
-        }
-    }
-    return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev: launch", hipGetErrorString(e));
-}
-#endif  // CIO_SHA1_WAVE_KERNEL
 
 // Chunks per workgroup for a batch of n: the fewest (8, then 16) whose grid
 // still fits one workgroup per CU, else the default geometry.
@@ -908,11 +593,6 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
     if (n > 0xFFFFFFFFull - 63) {
         return cioa_fail_msg("cio_sha1_batch_dev", "too many chunks for one launch");
     }
-#ifdef CIO_SHA1_WAVE_KERNEL
-    if (!dev_states && use_wave_kernel()) {
-        return sha1_wave_launch(reinterpret_cast<const uint8_t *>(dev_base), dev_offs, dev_lens, dev_digests, n, s);
-    }
-#endif
     const uint8_t *b = reinterpret_cast<const uint8_t *>(dev_base);
     auto launch = [&](auto geom) {
         using G = decltype(geom);

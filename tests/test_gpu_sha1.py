@@ -162,11 +162,10 @@ def test_select_free_groups(cuda, update):
 
 
 def test_block_count_boundaries(cuda):
-    """Block counts 1 .. 97 around multiples of 4 and 16 (the 32-chunk kernel's
-    4-block hand-over groups; the 16-block passes and 3-slot ring of the A/B
-    one-chunk-per-wave kernel, sha1_wave_kernel), cycled so that the chunks of
-    one workgroup end in different groups, aligned and misaligned, 1100
-    chunks (more workgroups than fit at once in the A/B kernel's grid)."""
+    """Block counts 1 .. 97 around multiples of 4 and 16 (the kernel's 4-block
+    hand-over groups), cycled so that the chunks of one workgroup end in
+    different groups, aligned and misaligned, 1100 chunks (more workgroups
+    than CUs at 8 chunks per workgroup)."""
     import torch
     rng = np.random.default_rng(25)
     nblks = [1, 15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 95, 96, 97]

@@ -255,68 +255,3 @@ def test_l64_chain_decomposition(nsteps, seed):
             s = po.crc_update(po.crc_shift(s, STEP - 64), blk)
         acc ^= po.crc_shift(s, 64 * (63 - L))
     assert acc == po.crc_update(seed, data)
-
-
-# ---- SHA-1 round routine of the A/B one-chunk-per-wave kernel ------------
-# tools/gen_sha1_wave_asm.py writes the round wave's loop as inline asm with
-# renamed state registers and a first-write-to-X scheme.  Emulating its VALU
-# lines on the CPU checks that register bookkeeping against hashlib.
-
-def _emulate_sha1_routine(message):
-    import importlib.util
-    import os
-    import struct
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location("gen", os.path.join(root, "tools", "gen_sha1_wave_asm.py"))
-    gen = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(gen)
-    lines = []
-    gen.block(lines)
-
-    def rotl(x, n):
-        return ((x << n) | (x >> (32 - n))) & 0xFFFFFFFF
-
-    K = (0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xCA62C1D6)
-    tables = {"0xca": lambda b, c, d: (b & c) | (~b & d),
-              "0x96": lambda b, c, d: b ^ c ^ d,
-              "0xe8": lambda b, c, d: (b & c) | (b & d) | (c & d)}
-    h = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
-    ml = len(message) * 8
-    msg = message + b"\x80" + b"\x00" * ((55 - len(message)) % 64) + struct.pack(">Q", ml)
-    for off in range(0, len(msg), 64):
-        w = list(struct.unpack(">16I", msg[off:off + 64]))
-        for t in range(16, 80):
-            w.append(rotl(w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16], 1))
-        kw = [(w[t] + K[t // 20]) & 0xFFFFFFFF for t in range(80)]
-        regs = {f"%[h{k}]": h[k] for k in range(5)}
-        # segment i of the block lives in buffer i's SGPRs (gen.sreg)
-        for t in range(80):
-            regs[gen.sreg(t // gen.SEG_WORDS, t % gen.SEG_WORDS)] = kw[t]
-        for ln in lines:
-            op, _, rest = ln.partition(" ")
-            if not op.startswith("v_"):
-                continue
-            args = [a.strip() for a in rest.split(",")]
-            if op == "v_bitop3_b32":
-                fn = args[3].split("bitop3:")[1]
-                args[3] = args[3].split()[0]
-                regs[args[0]] = tables[fn](regs[args[1]], regs[args[2]], regs[args[3]]) & 0xFFFFFFFF
-            elif op == "v_add_u32_e32":
-                regs[args[0]] = (regs[args[1]] + regs[args[2]]) & 0xFFFFFFFF
-            elif op == "v_add3_u32":
-                regs[args[0]] = (regs[args[1]] + regs[args[2]] + regs[args[3]]) & 0xFFFFFFFF
-            elif op == "v_alignbit_b32":
-                assert args[1] == args[2]
-                sh = int(args[3])
-                regs[args[0]] = ((regs[args[1]] >> sh) | (regs[args[1]] << (32 - sh))) & 0xFFFFFFFF
-            else:
-                raise AssertionError(op)
-        h = [regs[f"%[h{k}]"] for k in range(5)]
-    return b"".join(struct.pack(">I", x) for x in h)
-
-
-@pytest.mark.parametrize("n", [0, 3, 55, 56, 64, 119, 200, 1000])
-def test_sha1_wave_round_routine_emulated(n):
-    import hashlib
-    msg = bytes((7 * i + 3) & 0xFF for i in range(n))
-    assert _emulate_sha1_routine(msg) == hashlib.sha1(msg).digest()
