@@ -14,7 +14,7 @@ CFLAGS   := -O3 -fPIC -Wall -Wextra -std=gnu11 $(INC)
 HIPFLAGS := -O3 -fPIC --offload-arch=$(ARCH) -std=c++17 -Wall $(INC) -munsafe-fp-atomics \
             -mllvm -amdgpu-atomic-optimizer-strategy=None -mllvm -amdgpu-kernarg-preload-count=9
 
-COBJS   := $(BLD)/host_copy.o $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o $(BLD)/cioa_chunk.o $(BLD)/crc_route.o
+COBJS   := $(BLD)/host_copy.o $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o $(BLD)/cioa_chunk.o $(BLD)/crc_route.o $(BLD)/crc_cpu_batch.o
 HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/host_pipeline.o $(BLD)/sha1_gpu.o
 
 CTEST   := tests/c/bin

@@ -602,6 +602,7 @@ def run_e2e(args, rank, world, device, dist):
         cio.host_unregister(host)
     value_reg = int(lens.sum()) * world * steps / elapsed_reg / 1e9
     check = {"registered_equals_staged": bool(np.array_equal(out, out_reg))}
+    host_cpu = host_cpu_batch(host, offs, lens, out)
     if world == 1:
         import hashlib
         with open(os.path.join(ROOT, "tests", "golden", "crc32_vectors.json")) as f:
@@ -619,6 +620,7 @@ def run_e2e(args, rank, world, device, dist):
                                     "h2d_from_registered_pages_GBps": reg_h2d,
                                     "note": "host batch pinned once with cio_crc32_host_register "
                                             "(outside the timed loop); chunks DMA'd directly"},
+            "host_cpu_batch": host_cpu,
             "breakdown": e2e_breakdown(host, device),
             "pipe_legs_last_call": {"staged": legs_staged, "registered": legs_reg,
                                     "note": "cio_gpu_pipe_last_timing() after the last timed call: total = the "
@@ -628,6 +630,37 @@ def run_e2e(args, rank, world, device, dist):
                                             "total minus the DMA bound (bytes / pinned_h2d_GBps) is "
                                             "pipeline fill/drain and host overhead"},
             "check": check}
+
+
+def host_cpu_threads():
+    """Host threads for the library's host CRC legs: the box's CPU share per
+    GPU (16 on the MI355X box), at most this process's affinity."""
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    return max(1, min(16, share))
+
+
+def host_cpu_batch(host, offs, lens, gpu_out):
+    """The library's own host path over the same host batch (cio_crc32_batch_cpu:
+    crc_update with VPCLMULQDQ folding, 1 thread and the box's per-GPU CPU
+    share), next to the GPU host paths: which engine wins for host-resident
+    chunks (crc_route.c routes the chunk layer by this)."""
+    import chunkio_amd as cio
+    res = {}
+    for t in sorted({1, host_cpu_threads()}):
+        cio.crc32_batch_cpu_packed(host, offs, lens, threads=t)          # warm (pool, pages)
+        reps = 3 if t == 1 else 10
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = cio.crc32_batch_cpu_packed(host, offs, lens, threads=t)
+        dt = (time.perf_counter() - t0) / reps
+        res[f"threads_{t}"] = {"GBps": round(int(lens.sum()) / dt / 1e9, 2), "ms": round(dt * 1e3, 3),
+                               "equals_gpu": bool(np.array_equal(got, gpu_out))}
+    res["note"] = ("cio_crc32_batch_cpu over the same pageable host batch (DRAM-resident), min of "
+                   "back-to-back calls' mean; no PCIe")
+    return res
 
 
 def e2e_breakdown(host, device):
@@ -692,6 +725,27 @@ def run_perf(args, rank, world, device, dist, compact=False):
         return min(times), nb, hdr_ok
 
     t_def, nbytes, ok_def = timed(cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, "deferred")
+    # The same C layer in the reference's order (crc_update per write on the
+    # calling thread: VPCLMULQDQ folding over the cached 400 KB buffer), and
+    # deferred with the sync batches on the host (host threads granted, so the
+    # route puts them on the CPU pool): the library's own host paths beside
+    # the GPU sync, same run.
+    import chunkio_amd as cio
+    t_imm, _, ok_imm = timed(cf.CIO_CHECKSUM, "immediate")
+    nt = host_cpu_threads()
+    try:
+        cio.route(reset=True, threads=nt)
+        t_dh, _, ok_dh = timed(cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, "deferred-host")
+    finally:
+        cio.route(reset=True)
+    host_paths = {"c_layer_immediate": {"GBps": round(nbytes / t_imm / 1e9, 3), "ms": round(t_imm * 1e3, 2),
+                                        "threads": 1,
+                                        "note": "crc_update per write on the calling thread (reference order), "
+                                                "finalize per sync"},
+                  f"c_layer_deferred_host_{nt}t": {"GBps": round(nbytes / t_dh / 1e9, 3), "ms": round(t_dh * 1e3, 2),
+                                                    "threads": nt,
+                                                    "note": "appends only copy; each 100-chunk sync batch CRC'd by "
+                                                            "cio_crc32_batch_cpu on the host pool"}}
     if compact:
         return {"metric": "cio -k -p loop (1000 files x 5 x 400 KB, CRC32) GB/s with deferred CRC + batched "
                           "GPU sync", "value": round(nbytes / t_def / 1e9, 3), "unit": "GB/s", "steps": reps,
@@ -702,10 +756,10 @@ def run_perf(args, rank, world, device, dist, compact=False):
                 "config": {"workload": "config 1 loop through the C chunk layer (cioa_bench_perf_write): open, "
                                        "5 x write 409600 B, sync (batches of 100 chunks per GPU pass), close",
                            "files": files, "writes": writes, "sync_batch": batch},
-                "check": {"last_file_header_c100088740e7": bool(ok_def)},
+                "host_paths": host_paths,
+                "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm and ok_dh)},
                 "cpu_baseline_ref": "cpu_baseline.cio_perf_k_p of this line: the reference loop with the "
                                     "reference's own crc_update, same box, same run"}
-    t_imm, _, ok_imm = timed(cf.CIO_CHECKSUM, "immediate")
     from oracle import pyoracle as po
     lib = po.ref()
     kind, prefix = "reference", "ref_"
@@ -728,10 +782,8 @@ def run_perf(args, rank, world, device, dist, compact=False):
             "config": {"workload": "config 1 loop through the C chunk layer (cioa_bench_perf_write): open, "
                                    "5 x write 409600 B, sync (batches of 100 chunks per GPU pass), close",
                        "files": files, "writes": writes, "sync_batch": batch},
-            "c_layer_immediate": {"value": round(nbytes / t_imm / 1e9, 3), "unit": "GB/s",
-                                  "note": "same C layer, reference order: crc_update per write on the CPU, "
-                                          "finalize per sync"},
-            "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm)},
+            "host_paths": host_paths,
+            "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm and ok_dh)},
             "vs_baseline_note": "BASELINE.md's published `cio -k -p` rate, 545,507,660 B/s (README.md:120-129, "
                                 "hardware unstated)",
             "cpu_baseline": {"value": ref["crc_on"]["GBps"], "unit": "GB/s", "cores": 1, "kind": kind,
@@ -784,6 +836,30 @@ def run_verify(args, rank, world, device, dist, compact=False):
         check = {"good_files_ok": bool(np.all(st[ok_idx] == 0)),
                  "good_crc_088740e7": bool(np.all((cr[ok_idx] ^ 0xFFFFFFFF) == 0x088740E7)),
                  "flipped_file_bad_checksum": bool(st[bad] == -3 and er[bad] == -10)}
+        # The same call with the CRC pass on the host (crc_route.c): one
+        # thread (every batch forced to the host) and the box's per-GPU CPU
+        # share (host threads granted: the route's model puts every
+        # host-memory batch on the CPU).
+        import chunkio_amd as cio
+        host_route = {}
+        try:
+            for tag, kw in (("threads_1", {"cpu_max": -1, "threads": 1}),
+                            (f"threads_{host_cpu_threads()}", {"threads": host_cpu_threads()})):
+                cio.route(reset=True, **kw)
+                cf.verify_paths(paths)
+                ht = []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    st2, er2, cr2 = cf.verify_paths(paths)
+                    ht.append(time.perf_counter() - t0)
+                host_route[tag] = {"GBps": round(files * region / min(ht) / 1e9, 3),
+                                   "ms": round(min(ht) * 1e3, 3),
+                                   "same_results_as_gpu": bool(np.array_equal(st2, st) and np.array_equal(er2, er)
+                                                               and np.array_equal(cr2, cr))}
+        finally:
+            cio.route(reset=True)
+        host_route["note"] = ("cio_verify_paths with the CRC batch routed to the library's host crc_update "
+                              "(cio_crc32_batch_fd_cpu: pread + VPCLMULQDQ folding) instead of the GPU")
         cpu = None
         if rank == 0 and not args.no_cpu:
             import mmap
@@ -817,6 +893,7 @@ def run_verify(args, rank, world, device, dist, compact=False):
            "config": {"workload": "verify-on-load of 1000 x 2,068,480-B chunk files (CRC region "
                                   f"{region} B each), open/pread/close included", "files": files,
                       "file_bytes": fsize},
+           "host_route": host_route,
            "check": check}
     if cpu is not None:
         res["cpu_baseline"] = cpu
@@ -1041,6 +1118,7 @@ def other_configs(args, rank, world, device, dist):
         keep = {k: r[k] for k in ("metric", "value", "unit", "scaling", "steps", "warmup", "ms_per_step")}
         keep["workload"] = r["config"].get("workload")
         for k in ("roofline", "check", "per_gpu", "registered_in_place", "breakdown", "pipe_legs_last_call",
+                  "host_cpu_batch", "host_route", "host_paths",
                   "cpu_baseline", "cpu_baseline_ref", "vs_baseline", "vs_baseline_note"):
             if k in r:
                 keep[k] = r[k]

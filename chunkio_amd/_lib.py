@@ -23,7 +23,9 @@ EXPORTS = (
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_batch_dev", "cio_crc32_batch_host",
     "cio_crc32_batch_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device",
     "cio_crc32_host_register", "cio_crc32_host_unregister", "cio_gpu_pipe_last_timing",
-    "cio_crc32_cpu_max", "cio_crc32_set_cpu_max",
+    "cio_crc32_cpu_max", "cio_crc32_set_cpu_max", "cio_crc32_host_threads", "cio_crc32_set_host_threads",
+    "cio_crc32_route_reset",
+    "cio_crc32_batch_cpu", "cio_crc32_batch_fd_cpu",
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_sha1_batch_dev_async",
     "cio_sha1_state_init", "cio_sha1_update_batch_dev", "cio_sha1_final_batch_dev", "cio_gpu_read_stream",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
@@ -81,6 +83,13 @@ def _bind(lib):
         "cio_gpu_pipe_last_timing": (ctypes.c_int, [P(ctypes.c_double), ctypes.c_int]),
         "cio_crc32_cpu_max": (ctypes.c_size_t, []),
         "cio_crc32_set_cpu_max": (None, [ctypes.c_size_t]),
+        "cio_crc32_host_threads": (ctypes.c_int, []),
+        "cio_crc32_set_host_threads": (None, [ctypes.c_int]),
+        "cio_crc32_route_reset": (None, []),
+        "cio_crc32_batch_cpu": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p, ctypes.c_size_t,
+                                               ctypes.c_int]),
+        "cio_crc32_batch_fd_cpu": (ctypes.c_int, [P(ctypes.c_int), c_u64_p, P(ctypes.c_size_t), c_u32_p, c_u32_p,
+                                                  ctypes.c_size_t, ctypes.c_int]),
         "cio_gpu_fill_synthetic": (ctypes.c_int, [V, c_u64_p, c_u64_p, c_u64_p, ctypes.c_size_t,
                                                   ctypes.c_uint64, V]),
         "cio_sha1_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, ctypes.c_size_t, V]),

@@ -207,6 +207,52 @@ def crc32_batch_host_packed(host, offs, lens, seeds=None, devices=None):
     return out[:n]
 
 
+def crc32_batch_cpu_packed(host, offs, lens, seeds=None, threads=1):
+    """The same batch as crc32_batch_host_packed on the host CPU
+    (cio_crc32_batch_cpu: the library's crc_update on `threads` threads)."""
+    host = np.ascontiguousarray(host).view(np.uint8).reshape(-1)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    n = len(lens)
+    if n and int((offs + lens).max()) > host.size:
+        raise ValueError("crc32_batch_cpu_packed: chunk past the end of the host array")
+    ptrs = offs + np.uint64(host.ctypes.data)
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    seeds_p = None
+    if seeds is not None:
+        seeds_arr = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint32))
+        seeds_p = seeds_arr.ctypes.data_as(_lib.c_u32_p)
+    P = ctypes.POINTER
+    _lib.check(_lib.lib().cio_crc32_batch_cpu(ptrs.ctypes.data_as(P(ctypes.c_void_p)),
+                                              lens.ctypes.data_as(P(ctypes.c_size_t)), seeds_p,
+                                              out.ctypes.data_as(_lib.c_u32_p), n, int(threads)),
+               "cio_crc32_batch_cpu")
+    return out[:n]
+
+
+def host_threads(threads=None):
+    """The chunk layer's host CRC thread count (cio_crc32_host_threads); with
+    an argument, set it first (cio_crc32_set_host_threads)."""
+    if threads is not None:
+        _lib.lib().cio_crc32_set_host_threads(int(threads))
+    return int(_lib.lib().cio_crc32_host_threads())
+
+
+def route(cpu_max=None, threads=None, reset=False):
+    """The chunk layer's host/GPU route (crc_route.c): reset=True drops earlier
+    settings; cpu_max (bytes, -1 = every batch on the host) and threads set
+    the threshold and the host thread count.  Returns (cpu_max, threads) in
+    effect."""
+    lib = _lib.lib()
+    if reset:
+        lib.cio_crc32_route_reset()
+    if cpu_max is not None:
+        lib.cio_crc32_set_cpu_max(ctypes.c_size_t(cpu_max).value)
+    if threads is not None:
+        lib.cio_crc32_set_host_threads(int(threads))
+    return int(lib.cio_crc32_cpu_max()), int(lib.cio_crc32_host_threads())
+
+
 def device_count():
     """Visible GPUs (cio_gpu_device_count)."""
     return int(_lib.lib().cio_gpu_device_count())

@@ -1,27 +1,37 @@
 /*
  * crc_route.c -- where the chunk layer's host-memory CRCs run.
  *
- * A GPU pass over host memory (cio_crc32_batch_host_multi) has a fixed cost
- * per call: the plan image and the bytes go over PCIe, the kernel launches,
- * the states come back, and the caller waits on two synchronisations.  For
- * the single-chunk paths of chunkio's API -- the verify of one chunk on
- * open/up (src/cio_file.c:266-290), a full recompute after write_at or a
- * metadata move (:97-113), a deferred catch-up before a transaction -- and
- * for small batches, the library's own crc_update (crc32_host.c, the
- * drop-in for deps/crc32/crc32.c:337-390) on the calling thread finishes
- * first.  cioa_crc_batch_route() sends a batch whose total size is at most
- * cio_crc32_cpu_max() bytes there, and everything larger to the GPU.  The
- * default comes from the latency table in profiles/r03/crossover_r03b.txt
- * (tools/crossover.py on the GPU box): one chunk through the GPU host batch
- * costs 85 us at any size up to 4 KiB and 206 us at 2 MiB (its fixed cost,
- * then ~20 GB/s), while crc_update (VPCLMULQDQ folding, crc32_host.c) takes
- * 0.3 us at 16 B and 27 us at 2 MiB (~77 GB/s on cached data), so a single
- * chunk never pays for the round trip up to 8 MiB.  A batch of many chunks
- * streams through the pipelined GPU path at ~50 GB/s (PCIe-bound) against
- * one host thread's ~25 GB/s from DRAM: 85 us + B / 50 GB/s < B / 25 GB/s
- * from B ~ 4 MiB.  Results are identical either way (both compute
- * crc_update(seed, bytes)); the public cio_crc32_batch_* entry points never
- * route -- they are the GPU path.
+ * The chunk layer's verify/sync batches (cio_verify.c, cio_sync.c,
+ * cioa_chunk.c) hold chunk bytes in host memory (mmap'd files,
+ * src/cio_file_unix.c:100) or in files.  Two engines can CRC them, with
+ * identical results (both compute crc_update(seed, bytes)):
+ *
+ *   - the GPU host batch (cio_crc32_batch_host_multi / _fd_multi): a fixed
+ *     cost per call (plan image + bytes over PCIe, launches, the states back,
+ *     two synchronisations), then the PCIe rate per device;
+ *   - the host batch (cio_crc32_batch_cpu / _fd_cpu, crc_cpu_batch.c): the
+ *     library's crc_update (VPCLMULQDQ folding) on cio_crc32_host_threads()
+ *     threads, no fixed cost to speak of, a per-thread rate from DRAM up to
+ *     the socket's memory bandwidth.
+ *
+ * cioa_crc_batch_route() sends a batch whose total size is at most
+ * cio_crc32_cpu_max() bytes to the host, everything larger to the GPU.  The
+ * default threshold comes from that cost model with rates measured on the
+ * MI355X box (bench.py's `host_route` leg, profiles/r04/):
+ *
+ *   GPU:  kGpuFixedUs + B / (G x kGpuGBps)      G = distinct devices in the call
+ *   host: B / min(T x kCpuThreadGBps, kCpuMemGBps)
+ *
+ * so the host wins below B* = kGpuFixedUs / (1/r_host - 1/r_gpu), and for
+ * every size once r_host >= r_gpu.  With chunkio's one thread (T = 1, the
+ * default: the reference is single-threaded and so is Fluent Bit's caller)
+ * B* is ~4 MiB per device.  With T >= 2 host threads the host's DRAM rate
+ * already beats one PCIe link, so host-resident batches stay on the CPU: the
+ * GPU path pays off for host-resident chunks only when the caller cannot
+ * spare cores.  CIOA_CPU_CRC_MAX / cio_crc32_set_cpu_max() override the
+ * threshold (0 = always the GPU); CIOA_HOST_CRC_THREADS /
+ * cio_crc32_set_host_threads() set T.  The public cio_crc32_batch_* entry
+ * points never route.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -33,27 +43,84 @@
 #include "chunkio_amd/cio_crc32_gpu.h"
 #include "crc32_host.h"
 
-/* Bytes per call at or below which the host CRC is faster than a GPU round
- * trip (measured; see the header comment). */
-#define CIOA_CPU_CRC_MAX_DEFAULT ((size_t) 4 << 20)
+/* Cost-model rates (see the header comment). */
+static const double kGpuFixedUs = 85.0;      /* one-chunk GPU host batch at <= 4 KiB (crossover_r03b.txt) */
+static const double kGpuGBps = 47.0;         /* pipelined GPU host batch per device (bench e2e, staged) */
+static const double kCpuThreadGBps = 25.0;   /* crc_update, one thread, DRAM-resident */
+static const double kCpuMemGBps = 200.0;     /* host threads together, DRAM-resident */
 
 static size_t g_cpu_max;
 static int g_cpu_max_set;
+static int g_threads;
+static int g_threads_set;
 
-size_t cio_crc32_cpu_max(void)
+int cio_crc32_host_threads(void)
+{
+    if (__atomic_load_n(&g_threads_set, __ATOMIC_ACQUIRE)) {
+        return __atomic_load_n(&g_threads, __ATOMIC_RELAXED);
+    }
+    const char *r = getenv("CIOA_HOST_CRC_THREADS");
+    if (r && *r) {
+        const int v = atoi(r);
+        if (v >= 1 && v <= 64) {
+            return v;
+        }
+    }
+    return 1;
+}
+
+void cio_crc32_set_host_threads(int threads)
+{
+    if (threads < 1) {
+        threads = 1;
+    }
+    if (threads > 64) {
+        threads = 64;
+    }
+    __atomic_store_n(&g_threads, threads, __ATOMIC_RELAXED);
+    __atomic_store_n(&g_threads_set, 1, __ATOMIC_RELEASE);
+}
+
+/* The model's crossover for T host threads against G devices. */
+static size_t model_cpu_max(int threads, int ndev)
+{
+    double r_host = threads * kCpuThreadGBps;
+    if (r_host > kCpuMemGBps) {
+        r_host = kCpuMemGBps;
+    }
+    const double r_gpu = (ndev > 1 ? ndev : 1) * kGpuGBps;
+    if (r_host >= r_gpu) {
+        return SIZE_MAX;
+    }
+    const double b = kGpuFixedUs * 1e-6 / (1.0 / (r_host * 1e9) - 1.0 / (r_gpu * 1e9));
+    return (size_t) b;
+}
+
+static int explicit_cpu_max(size_t *out)
 {
     if (__atomic_load_n(&g_cpu_max_set, __ATOMIC_ACQUIRE)) {
-        return __atomic_load_n(&g_cpu_max, __ATOMIC_RELAXED);
+        *out = __atomic_load_n(&g_cpu_max, __ATOMIC_RELAXED);
+        return 1;
     }
     const char *r = getenv("CIOA_CPU_CRC_MAX");
     if (r && *r) {
         char *end = NULL;
         const unsigned long long v = strtoull(r, &end, 10);
         if (end && *end == '\0') {
-            return (size_t) v;
+            *out = (size_t) v;
+            return 1;
         }
     }
-    return CIOA_CPU_CRC_MAX_DEFAULT;
+    return 0;
+}
+
+size_t cio_crc32_cpu_max(void)
+{
+    size_t v;
+    if (explicit_cpu_max(&v)) {
+        return v;
+    }
+    return model_cpu_max(cio_crc32_host_threads(), 1);
 }
 
 void cio_crc32_set_cpu_max(size_t bytes)
@@ -62,9 +129,32 @@ void cio_crc32_set_cpu_max(size_t bytes)
     __atomic_store_n(&g_cpu_max_set, 1, __ATOMIC_RELEASE);
 }
 
-static int route_to_cpu(const size_t *lens, size_t n)
+void cio_crc32_route_reset(void)
 {
-    const size_t max = cio_crc32_cpu_max();
+    __atomic_store_n(&g_cpu_max_set, 0, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_threads_set, 0, __ATOMIC_RELEASE);
+}
+
+/* Distinct device ordinals in a *_multi device list (1 for the current device). */
+static int distinct_devices(const int *devices, int ndev)
+{
+    int k = 0;
+    for (int a = 0; a < ndev; a++) {
+        int seen = 0;
+        for (int b = 0; b < a && !seen; b++) {
+            seen = devices[b] == devices[a];
+        }
+        k += !seen;
+    }
+    return k > 0 ? k : 1;
+}
+
+static int route_to_cpu(const size_t *lens, size_t n, const int *devices, int ndev)
+{
+    size_t max;
+    if (!explicit_cpu_max(&max)) {
+        max = model_cpu_max(cio_crc32_host_threads(), devices ? distinct_devices(devices, ndev) : 1);
+    }
     size_t total = 0;
     for (size_t i = 0; i < n; i++) {
         total += lens[i];
@@ -81,49 +171,20 @@ int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint
     if (n == 0) {
         return CIO_OK;
     }
-    if (!route_to_cpu(lens, n)) {
+    if (!route_to_cpu(lens, n, devices, ndev)) {
         return cio_crc32_batch_host_multi(bufs, lens, seeds, out_raw, n, devices, ndev);
     }
-    for (size_t i = 0; i < n; i++) {
-        const uint32_t s = seeds ? seeds[i] : 0xffffffffu;
-        out_raw[i] = (uint32_t) crc_update((crc_t) s, bufs[i], lens[i]);
-    }
-    return CIO_OK;
+    return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
 }
 
 int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens, const uint32_t *seeds,
                       uint32_t *out_raw, size_t n, const int *devices, int ndev)
 {
-    enum { PIECE = 256 << 10 };
     if (n == 0) {
         return CIO_OK;
     }
-    if (!route_to_cpu(lens, n)) {
+    if (!route_to_cpu(lens, n, devices, ndev)) {
         return cio_crc32_batch_fd_multi(fds, foffs, lens, seeds, out_raw, n, devices, ndev);
     }
-    unsigned char *buf = malloc(PIECE);
-    if (!buf) {
-        return cioa_fail_msg("cioa_crc_fd_route", "out of memory");
-    }
-    int rc = CIO_OK;
-    for (size_t i = 0; i < n && rc == CIO_OK; i++) {
-        crc_t c = (crc_t) (seeds ? seeds[i] : 0xffffffffu);
-        size_t done = 0;
-        while (done < lens[i]) {
-            const size_t want = lens[i] - done < PIECE ? lens[i] - done : PIECE;
-            const ssize_t r = pread(fds[i], buf, want, (off_t) (foffs[i] + done));
-            if (r < 0 && errno == EINTR) {
-                continue;
-            }
-            if (r <= 0) {
-                rc = cioa_fail_msg("cioa_crc_fd_route", "short read from a file source");
-                break;
-            }
-            c = crc_update(c, buf, (size_t) r);
-            done += (size_t) r;
-        }
-        out_raw[i] = (uint32_t) c;
-    }
-    free(buf);
-    return rc;
+    return cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads());
 }

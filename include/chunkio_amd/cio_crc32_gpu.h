@@ -172,19 +172,42 @@ int  cio_crc32_host_unregister(const void *p);
  * builds ms, staging groups, staged bytes.  Fills min(n, 6) values. */
 int  cio_gpu_pipe_last_timing(double *out, int n);
 
-/* Small-batch routing of the chunk layer.  The verify/sync batches
- * (cio_verify.h, cio_sync.h) and the chunk API (cioa_chunk.h) compute a
- * batch whose regions total at most cio_crc32_cpu_max() bytes with the
- * library's crc_update on the calling thread instead of a GPU round trip
- * (one chunk's verify on open/up, a recompute after write_at, a deferred
- * catch-up); larger batches take the GPU path above.  Same results either
- * way.  The default is the measured crossover of one-chunk GPU host batches
- * against crc_update (profiles/r03/crossover_*.txt); the environment
- * variable CIOA_CPU_CRC_MAX (bytes) or cio_crc32_set_cpu_max() overrides it,
- * 0 sends everything to the GPU.  The cio_crc32_batch_* entry points above
- * never route: they always run on the GPU. */
+/* ---- batched CRC-32 on the host CPU ------------------------------------ */
+
+/* The same batch as cio_crc32_batch_host / _fd_multi computed on the host:
+ * crc_update (the library's drop-in for deps/crc32/crc32.c:337-390) on up to
+ * `threads` threads of a persistent pool (the calling thread included).
+ * Chunks above 1 MiB are split into pieces and folded with
+ * cio_crc32_combine, so one large chunk uses every thread; small chunks are
+ * grouped.  threads <= 1 is the reference's own loop on the calling thread.
+ * Results are bit-identical to the GPU batch.  One batch runs in the pool at
+ * a time (concurrent callers queue). */
+int  cio_crc32_batch_cpu(const void *const *bufs, const size_t *lens,
+                         const uint32_t *seeds, uint32_t *out_raw, size_t n,
+                         int threads);
+int  cio_crc32_batch_fd_cpu(const int *fds, const uint64_t *foffs, const size_t *lens,
+                            const uint32_t *seeds, uint32_t *out_raw, size_t n,
+                            int threads);
+
+/* Routing of the chunk layer's CRCs over host memory.  The verify/sync
+ * batches (cio_verify.h, cio_sync.h) and the chunk API (cioa_chunk.h) compute
+ * a batch whose regions total at most cio_crc32_cpu_max() bytes on the host
+ * (cio_crc32_batch_cpu with cio_crc32_host_threads() threads) and larger
+ * batches on the GPU (cio_crc32_batch_host_multi / _fd_multi).  Same results
+ * either way.  The default threshold is a cost model with rates measured on
+ * the MI355X box (crc_route.c): with the default single host thread it is
+ * ~4 MiB per device in the call's device list; with two or more host threads
+ * the host's DRAM rate beats a PCIe link and every host-memory batch stays on
+ * the CPU.  CIOA_CPU_CRC_MAX (bytes) or cio_crc32_set_cpu_max() override the
+ * threshold, 0 sends everything to the GPU; CIOA_HOST_CRC_THREADS or
+ * cio_crc32_set_host_threads() (1..64) set the thread count.  The
+ * cio_crc32_batch_* entry points never route. */
 size_t cio_crc32_cpu_max(void);
 void   cio_crc32_set_cpu_max(size_t bytes);
+int    cio_crc32_host_threads(void);
+void   cio_crc32_set_host_threads(int threads);
+/* Drop what the two setters set (back to the environment / defaults). */
+void   cio_crc32_route_reset(void);
 
 /* ---- synthetic data (benchmarks / tests) ------------------------------- */
 

@@ -8,10 +8,12 @@
  * every append's critical path.
  *
  * With the CRC deferred, appends only copy; cio_file_sync_batch() then brings
- * N dirty chunks up to date in ONE batched GPU pass: for each chunk the bytes
+ * N dirty chunks up to date in ONE batch: for each chunk the bytes
  * [crc_end, 24 + meta_len + content_len) not yet covered are CRC'd with
- * crc_cur as the seed (crc_update(crc_cur, ...), cio_crc32_batch_host), and
- * the header is written exactly as the reference would have left it:
+ * crc_cur as the seed (crc_update(crc_cur, ...)) on the GPU
+ * (cio_crc32_batch_host_multi) or, when the batch routes to the host
+ * (cio_crc32_cpu_max(), cio_crc32_gpu.h), on the host's crc_update; and the
+ * header is written exactly as the reference would have left it:
  *
  *   CIOA_SYNC_FINALIZE: htonl(crc_finalize(crc)) in an 8-byte crc_t at map+2
  *                       (bytes 2..5 = big-endian CRC, 6..9 = 0), cio_file.c:116-124

@@ -1,13 +1,15 @@
 /*
- * cio_verify.h -- batched verify-on-load of chunkio chunk files on the GPU.
+ * cio_verify.h -- batched verify-on-load of chunkio chunk files.
  *
  * chunkio verifies a chunk when it maps an existing file: cio_scan_stream_files
  * (src/cio_scan.c:105) -> cio_chunk_open -> cio_file_open -> mmap_file
  * (src/cio_file.c:345-493) -> cio_file_format_check (src/cio_file.c:187-294).
  * One chunk at a time, single-threaded.  cio_file_verify_batch() runs the same
- * checks over N mapped chunk files and computes all their CRCs in ONE batched
- * GPU pass (cio_crc32_batch_host), returning per chunk exactly what the
- * reference would have recorded:
+ * checks over N mapped chunk files and computes all their CRCs in ONE batch
+ * -- on the GPU (cio_crc32_batch_host_multi), or on the host's crc_update
+ * when the batch routes there (cio_crc32_cpu_max(): small batches, or any
+ * batch when host CRC threads are granted, cio_crc32_gpu.h) -- returning per
+ * chunk exactly what the reference would have recorded:
  *
  *   magic bytes C1 00                        else CIO_ERR_BAD_LAYOUT     (cio_file.c:230-236)
  *   content length (BE u32 @10), legacy       else CIO_ERR_BAD_FILE_SIZE  (cio_file_st.h:129-179,

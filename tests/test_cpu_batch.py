@@ -1,0 +1,157 @@
+"""The host CRC batch (cio_crc32_batch_cpu / _fd_cpu, crc_cpu_batch.c) and the
+chunk layer's route between it and the GPU (crc_route.c).  CPU only: the host
+batch is the library's crc_update spread over a thread pool, checked here
+against the oracle (the reference's crc32.c restated, oracle/) bit for bit."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import chunkio_amd as cio
+from chunkio_amd import workloads as wl
+from oracle import pyoracle as po
+
+INIT = 0xFFFFFFFF
+
+
+def _batch(seed, lens):
+    lens = np.asarray(lens, dtype=np.uint64)
+    buf, offs = wl.host_batch(seed, lens)
+    return buf, offs, lens
+
+
+@pytest.mark.parametrize("threads", [1, 2, 3, 8, 16])
+def test_cpu_batch_matches_oracle(threads):
+    # empty, tiny, piece-boundary (1 MiB) and multi-piece chunks, interleaved
+    lens = [0, 1, 7, 4096, 409600, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, 3 * (1 << 20) + 5, 0, 12345] * 3
+    buf, offs, lens = _batch(0xC0FFEE, lens)
+    got = cio.crc32_batch_cpu_packed(buf, offs, lens, threads=threads)
+    np.testing.assert_array_equal(got, po.crc_batch(buf, offs, lens))
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_cpu_batch_seeds(threads):
+    lens = np.asarray([0, 3, 5000, 2 * (1 << 20) + 77, 64], np.uint64)
+    buf, offs, lens = _batch(0xABC, lens)
+    seeds = np.asarray([0, 0xBE26ED00, 0x12345678, 0xDEADBEEF, INIT], np.uint32)
+    got = cio.crc32_batch_cpu_packed(buf, offs, lens, seeds=seeds, threads=threads)
+    want = [po.crc_update(int(s), buf[int(o):int(o + n)]) for s, o, n in zip(seeds, offs, lens)]
+    np.testing.assert_array_equal(got, np.asarray(want, np.uint32))
+
+
+def test_cpu_batch_one_large_chunk_uses_pieces():
+    """A single 9 MiB + 3 chunk at a misaligned offset: 10 pieces folded with
+    cio_crc32_combine must equal one crc_update over the whole chunk."""
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 9 * (1 << 20) + 3 + 5, dtype=np.uint8)
+    offs = np.asarray([5], np.uint64)
+    lens = np.asarray([9 * (1 << 20) + 3], np.uint64)
+    for t in (1, 2, 7, 16):
+        got = cio.crc32_batch_cpu_packed(data, offs, lens, threads=t)
+        assert int(got[0]) == po.crc_update(INIT, data[5:])
+
+
+def test_cpu_batch_many_small_chunks_grouped():
+    lens = np.full(20000, 100, np.uint64)
+    lens[::7] = 0
+    buf, offs, lens = _batch(0x77, lens)
+    got = cio.crc32_batch_cpu_packed(buf, offs, lens, threads=16)
+    np.testing.assert_array_equal(got, po.crc_batch(buf, offs, lens))
+
+
+def test_cpu_batch_repeated_calls_and_thread_growth():
+    """The persistent pool: calls with growing and shrinking thread counts
+    (workers started for one call join it; idle ones sit out)."""
+    buf, offs, lens = _batch(0x99, [300000] * 40)
+    want = po.crc_batch(buf, offs, lens)
+    for t in (2, 5, 3, 16, 1, 9, 16, 2):
+        np.testing.assert_array_equal(cio.crc32_batch_cpu_packed(buf, offs, lens, threads=t), want)
+
+
+def test_cpu_batch_concurrent_callers():
+    import threading
+    buf, offs, lens = _batch(0x31, [700000] * 16)
+    want = po.crc_batch(buf, offs, lens)
+    errs = []
+
+    def run(t):
+        try:
+            for _ in range(5):
+                np.testing.assert_array_equal(cio.crc32_batch_cpu_packed(buf, offs, lens, threads=t), want)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(t,)) for t in (4, 8, 1, 16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+
+
+def _fd_cpu(fds, foffs, lens, threads):
+    n = len(lens)
+    P = ctypes.POINTER
+    fds_a = (ctypes.c_int * max(n, 1))(*fds)
+    fo = np.ascontiguousarray(foffs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    out = np.zeros(max(n, 1), np.uint32)
+    rc = cio.lib().cio_crc32_batch_fd_cpu(fds_a, fo.ctypes.data_as(P(ctypes.c_uint64)),
+                                          ln.ctypes.data_as(P(ctypes.c_size_t)), None,
+                                          out.ctypes.data_as(P(ctypes.c_uint32)), n, threads)
+    return rc, out[:n]
+
+
+@pytest.mark.parametrize("threads", [1, 6])
+def test_fd_cpu_batch(tmp_path, threads):
+    rng = np.random.default_rng(11)
+    paths, fds, foffs, lens, want = [], [], [], [], []
+    for i, n in enumerate([0, 10, 1 << 20, 2_500_001, 409600]):
+        data = rng.integers(0, 256, n + 22, dtype=np.uint8)
+        p = tmp_path / f"c{i}"
+        p.write_bytes(data.tobytes())
+        paths.append(p)
+        fds.append(os.open(p, os.O_RDONLY))
+        foffs.append(22)
+        lens.append(n)
+        want.append(po.crc_update(INIT, data[22:]))
+    try:
+        rc, got = _fd_cpu(fds, foffs, lens, threads)
+        assert rc == 0
+        np.testing.assert_array_equal(got, np.asarray(want, np.uint32))
+        # a range past the end of its file is a short read: CIO_ERROR
+        rc, _ = _fd_cpu(fds, foffs, [lens[0], lens[1] + 5, lens[2], lens[3], lens[4]], threads)
+        assert rc == -1
+        assert b"short read" in cio.lib().cio_gpu_last_error()
+    finally:
+        for fd in fds:
+            os.close(fd)
+
+
+def test_route_threshold_follows_host_threads():
+    """cio_crc32_cpu_max(): the cost model's crossover -- ~4 MiB with one host
+    thread, everything on the host with two or more (the host's DRAM rate
+    beats one PCIe link); an explicit threshold overrides the model."""
+    lib = cio.lib()
+    if os.environ.get("CIOA_CPU_CRC_MAX") or os.environ.get("CIOA_HOST_CRC_THREADS"):
+        pytest.skip("routing environment set by the caller")
+    before_max, before_t = cio.route()
+    model_max = cio.route(reset=True)[0]
+    try:
+        assert cio.host_threads(1) == 1
+        one = lib.cio_crc32_cpu_max()
+        assert 2 << 20 <= one <= 8 << 20, one
+        assert cio.host_threads(16) == 16
+        assert lib.cio_crc32_cpu_max() == ctypes.c_size_t(-1).value
+        assert cio.host_threads(0) == 1          # clamped
+        assert cio.host_threads(1000) == 64
+        # an explicit threshold overrides the model, reset drops it again
+        assert cio.route(cpu_max=12345)[0] == 12345
+        assert cio.route(reset=True) == (model_max, 1)
+    finally:
+        cio.route(reset=True)
+        if before_max != model_max:
+            cio.route(cpu_max=before_max)
+        if before_t != 1:
+            cio.route(threads=before_t)
