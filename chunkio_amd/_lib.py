@@ -113,6 +113,40 @@ def _bind(lib):
     return lib
 
 
+def _elf_dynamic_strings(path):
+    """(SONAME, [NEEDED...]) of a 64-bit little-endian ELF shared object, read
+    from its dynamic section; (None, []) if the file cannot be parsed."""
+    import struct
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+        if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+            return None, []
+        shoff, = struct.unpack_from("<Q", data, 0x28)
+        shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+        secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+        dyn = [sec for sec in secs if sec[1] == 6]           # SHT_DYNAMIC
+        if not dyn:
+            return None, []
+        _, _, _, _, off, size, link, _, _, _ = dyn[0]
+        stroff = secs[link][4]
+
+        def cstr(o):
+            return data[stroff + o:data.index(b"\0", stroff + o)].decode()
+        soname, needed = None, []
+        for k in range(size // 16):
+            tag, val = struct.unpack_from("<qQ", data, off + 16 * k)
+            if tag == 0:
+                break
+            if tag == 1:
+                needed.append(cstr(val))
+            elif tag == 14:
+                soname = cstr(val)
+        return soname, needed
+    except (OSError, ValueError, IndexError, struct.error):
+        return None, []
+
+
 def _pin_hip_runtime():
     """Make the library share ONE HIP runtime with torch in this process.
 
@@ -135,6 +169,18 @@ def _pin_hip_runtime():
             return None
         path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
         if not os.path.exists(path):
+            return None
+        # Pin torch's copy only if it IS the runtime this library links: same
+        # SONAME as the library's libamdhip64 DT_NEEDED entry.  A torch built
+        # against another major version would otherwise add a second runtime
+        # (and one this library never uses).
+        soname, _ = _elf_dynamic_strings(path)
+        _, needed = _elf_dynamic_strings(LIB_PATH)
+        want = [x for x in needed if x.startswith("libamdhip64")]
+        if soname is None or not want or soname not in want:
+            import warnings
+            warnings.warn(f"chunkio_amd: not pinning {path} (SONAME {soname}) for {LIB_PATH} "
+                          f"(needs {want or 'no libamdhip64'}); load torch first if both are used")
             return None
     return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 

@@ -352,6 +352,9 @@ def sha1_final_batch_dev(states, n=None, stream=None):
     """SHA1_Final of every context (left unchanged): n x 20 digest bytes (numpy)."""
     import torch
     n = states.numel() // SHA1_STATE_BYTES if n is None else n
+    if n < 0 or states.numel() < n * SHA1_STATE_BYTES:
+        raise ValueError(f"sha1_final_batch_dev: {n} contexts but states holds "
+                         f"{states.numel() // SHA1_STATE_BYTES}")
     out = torch.empty(max(n, 1) * 20, dtype=torch.uint8, device=states.device)
     _lib.check(_lib.lib().cio_sha1_final_batch_dev(_ptr(states), _ptr(out), n, _stream_ptr(stream)),
                "cio_sha1_final_batch_dev")

@@ -73,6 +73,29 @@ static size_t first_stage_bytes()
     }();
     return v;
 }
+// Streamed staging (default): a group's host copy is cut into sub-blocks of
+// CIO_GPU_DMA_SUB_MB MiB (default 4; 0 = one DMA per group after its whole
+// copy, the round-3 pipeline), and each sub-block's H2D DMA is queued as soon
+// as its bytes are in pinned memory.  The host copy (~63 GB/s with a DMA in
+// flight) outruns the link (~57 GB/s), so the DMA engine starts one
+// sub-block after the call begins and then never waits for a copy; groups
+// need not start small (they are all kStage) and no group's copy sits
+// between two DMAs.
+static size_t dma_sub_bytes()
+{
+    static const size_t v = [] {
+        long mb = 4;
+        if (const char *r = getenv("CIO_GPU_DMA_SUB_MB")) {
+            mb = atol(r);
+            if (mb < 0 || mb > 1024) {
+                mb = 4;
+            }
+        }
+        return (size_t) mb << 20;
+    }();
+    return v;
+}
+
 #ifdef CIO_PIPE_SLOTS
 constexpr int kSlots = CIO_PIPE_SLOTS;   // A/B builds only
 #else
@@ -170,6 +193,60 @@ public:
         return ok && !failed_;
     }
 
+    // Streamed form: the group's bytes in sub-blocks of `sub` bytes (a
+    // multiple of the piece size).  The workers copy pieces in order; the
+    // caller runs `before`, then `issue(lo, hi)` for each sub-block in order
+    // as soon as every piece of it is in dst (the DMA of a sub-block starts
+    // while later ones are still being copied).  With no workers the caller
+    // copies and issues alone.
+    template <typename F, typename I>
+    bool copy_streamed(uint8_t *dst, const HostGroup &g, uint64_t sub, F before, I issue)
+    {
+        const uint64_t piece = std::min<uint64_t>(sub / 16 ? sub / 16 : sub, kPieceMax);
+        const uint64_t nsub = (g.bytes + sub - 1) / sub;
+        const uint64_t npieces = (g.bytes + piece - 1) / piece;
+        if (workers_.empty() || npieces <= 1) {
+            before();
+            const bool ok = range(dst, g, 0, g.bytes);
+            cioa_stage_fence();
+            for (uint64_t k = 0; k < nsub; k++) {
+                issue(k * sub, std::min<uint64_t>(g.bytes, (k + 1) * sub));
+            }
+            return ok;
+        }
+        const uint64_t per_sub = sub / piece;
+        sub_left_.reset(new std::atomic<uint32_t>[nsub]);
+        for (uint64_t k = 0; k < nsub; k++) {
+            const uint64_t lo = k * per_sub, hi = std::min(npieces, (k + 1) * per_sub);
+            sub_left_[k].store((uint32_t) (hi - lo), std::memory_order_relaxed);
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            dst_ = dst;
+            g_ = &g;
+            npieces_ = npieces;
+            piece_ = piece;
+            per_sub_ = per_sub;
+            next_.store(0, std::memory_order_relaxed);
+            pending_ = workers_.size();
+            failed_ = false;
+            ++gen_;
+        }
+        cv_.notify_all();
+        before();
+        for (uint64_t k = 0; k < nsub; k++) {
+            // the workers finish sub-blocks at ~4 MiB / 60 GB/s = ~70 us each
+            while (sub_left_[k].load(std::memory_order_acquire) != 0) {
+                __builtin_ia32_pause();
+            }
+            issue(k * sub, std::min<uint64_t>(g.bytes, (k + 1) * sub));
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return pending_ == 0; });
+        per_sub_ = 0;
+        return !failed_;
+    }
+
 private:
     bool drain(uint8_t *dst, const HostGroup &g, uint64_t npieces, uint64_t piece)
     {
@@ -180,6 +257,11 @@ private:
                 return ok;
             }
             ok &= range(dst, g, p * piece, std::min<uint64_t>(g.bytes, (p + 1) * piece));
+            if (per_sub_) {
+                // publish the piece's streaming stores before its sub-block's count
+                cioa_stage_fence();
+                sub_left_[p / per_sub_].fetch_sub(1, std::memory_order_release);
+            }
         }
     }
     static constexpr uint64_t kBounce = 256u << 10;
@@ -269,6 +351,8 @@ private:
     uint64_t piece_ = kPieceMax;
     std::atomic<uint64_t> next_{0};
     size_t pending_ = 0;
+    uint64_t per_sub_ = 0;                               // pieces per sub-block (0: not streamed)
+    std::unique_ptr<std::atomic<uint32_t>[]> sub_left_;  // pieces still to copy per sub-block
 };
 
 size_t align256(size_t x)
@@ -532,10 +616,13 @@ hipError_t dma_registered(const HostGroup &g, uint8_t *dbuf, hipStream_t stream)
     return hipSuccess;
 }
 
-// The host legs of the last host batch (any thread, any device), for
-// cio_gpu_pipe_last_timing().
+// The host legs of host batches, for cio_gpu_pipe_last_timing(): the calling
+// thread's own last single-device batch, and the last one any thread
+// finished (what a *_multi caller sees: its devices run on internal threads,
+// so the record is the device pipeline that finished last).
 struct PipeTiming {
     double total_ms = 0, copy_ms = 0, slot_wait_ms = 0, plan_ms = 0, groups = 0, bytes = 0;
+    bool valid = false;
 };
 std::mutex g_timing_mu;
 PipeTiming g_last_timing;
@@ -564,7 +651,8 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     // first groups are smaller (first_stage_bytes(), doubling up to kStage):
     // the DMA engine starts after a short copy instead of a full slot's.
     std::vector<HostGroup> groups(1);
-    uint64_t cap = std::min<uint64_t>(first_stage_bytes(), kStage);
+    const uint64_t sub = dma_sub_bytes();
+    uint64_t cap = sub && !getenv("CIO_GPU_STAGE_FIRST_MB") ? kStage : std::min<uint64_t>(first_stage_bytes(), kStage);
     for (size_t i = 0; i < n; i++) {
         const uint8_t *p = fds ? nullptr : reinterpret_cast<const uint8_t *>(bufs[i]);
         uint64_t left = lens[i], done = 0;
@@ -658,6 +746,38 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
             // the metadata copy and the kernel on this stream).
             if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
             build();
+        } else if (sub) {
+            // staged, streamed: the plan is built while the copy workers fill
+            // the slot, then each sub-block's DMA is queued as soon as it is
+            // copied (the plan image goes first: it is ready before them)
+            const double tc = timing ? wall_s() : 0;
+            bool meta_sent = false;
+            hipError_t ed = hipSuccess;
+            const bool ok = hp->pool->copy_streamed(s.pinned, g, sub, build, [&](uint64_t lo, uint64_t hi) {
+                if (ed != hipSuccess || e != hipSuccess || err) {
+                    return;
+                }
+                if (!meta_sent) {
+                    ed = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream);
+                    meta_sent = true;
+                }
+                if (ed == hipSuccess) {
+                    ed = hipMemcpyAsync(s.dbuf + lo, s.pinned + lo, hi - lo, hipMemcpyHostToDevice, s.stream);
+                }
+            });
+            if (timing) {
+                t_copy += wall_s() - tc;
+            }
+            if (!ok) {
+                rc = fail("cio_crc32_batch: short read from a file source");
+                break;
+            }
+            if (e == hipSuccess) {
+                e = ed;
+            }
+            if (e == hipSuccess && !err && !meta_sent) {
+                e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream);
+            }
         } else {
             // staged: the plan is built while the copy workers fill the slot
             const double tc = timing ? wall_s() : 0;
@@ -674,8 +794,10 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
             rc = fail(err);
             break;
         }
-        if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
-        if (!direct) {
+        if (direct || !sub) {
+            if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
+        }
+        if (!direct && !sub) {
             if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
         }
         if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
@@ -710,6 +832,7 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
         pt.plan_ms = t_plan * 1e3;
         pt.groups = (double) groups.size();
         pt.bytes = (double) total;
+        pt.valid = true;
         if (print_timing) {
             fprintf(stderr, "batch_host: dev %d, %zu chunks, %zu groups, %.1f MB: total %.2f ms, copy %.2f ms, "
                             "slot waits %.2f ms, plans %.2f ms\n", dev, n, groups.size(), total / 1e6,
@@ -951,8 +1074,8 @@ extern "C" int cio_gpu_pipe_last_timing(double *out, int n)
     if (!out || n <= 0) {
         return fail("cio_gpu_pipe_last_timing: null argument");
     }
-    PipeTiming pt;
-    {
+    PipeTiming pt = t_last_timing;
+    if (!pt.valid) {
         std::lock_guard<std::mutex> lk(g_timing_mu);
         pt = g_last_timing;
     }

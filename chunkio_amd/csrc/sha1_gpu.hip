@@ -588,10 +588,10 @@ int sha1_chunks_per_wg(size_t n)
 }
 
 int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *dev_lens, uint8_t *dev_digests,
-                cio_sha1_state *dev_states, size_t n, hipStream_t s)
+                cio_sha1_state *dev_states, size_t n, hipStream_t s, const char *what)
 {
     if (n > 0xFFFFFFFFull - 63) {
-        return cioa_fail_msg("cio_sha1_batch_dev", "too many chunks for one launch");
+        return cioa_fail_msg(what, "too many chunks for one launch");
     }
     const uint8_t *b = reinterpret_cast<const uint8_t *>(dev_base);
     auto launch = [&](auto geom) {
@@ -614,7 +614,7 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
         launch(ShaGeomWide());
     }
     const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? CIO_OK : cioa_fail_msg("cio_sha1_batch_dev: launch", hipGetErrorString(e));
+    return e == hipSuccess ? CIO_OK : cioa_fail_msg(what, hipGetErrorString(e));
 }
 
 }  // namespace
@@ -657,7 +657,8 @@ extern "C" int cio_sha1_update_batch_dev(const void *dev_base, const uint64_t *d
     if (cio_gpu_init() != CIO_OK) {
         return CIO_ERROR;
     }
-    return sha1_launch(dev_base, dev_offs, dev_lens, nullptr, dev_states, n, reinterpret_cast<hipStream_t>(stream));
+    return sha1_launch(dev_base, dev_offs, dev_lens, nullptr, dev_states, n, reinterpret_cast<hipStream_t>(stream),
+                       "cio_sha1_update_batch_dev: launch");
 }
 
 extern "C" int cio_sha1_final_batch_dev(const cio_sha1_state *dev_states, uint8_t *dev_digests, size_t n,
@@ -693,7 +694,8 @@ extern "C" int cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *de
     if (cio_gpu_init() != CIO_OK) {
         return CIO_ERROR;
     }
-    return sha1_launch(dev_base, dev_offs, dev_lens, dev_digests, nullptr, n, reinterpret_cast<hipStream_t>(stream));
+    return sha1_launch(dev_base, dev_offs, dev_lens, dev_digests, nullptr, n, reinterpret_cast<hipStream_t>(stream),
+                       "cio_sha1_batch_dev_async: launch");
 }
 
 extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, const uint64_t *lens,
@@ -722,7 +724,7 @@ extern "C" int cio_sha1_batch_dev(const void *dev_base, const uint64_t *offs, co
         (void) hipFree(d);
         return cioa_fail_msg("cio_sha1_batch_dev: copy", hipGetErrorString(e));
     }
-    const int rc = sha1_launch(dev_base, d, d + n, dev_digests, nullptr, n, s);
+    const int rc = sha1_launch(dev_base, d, d + n, dev_digests, nullptr, n, s, "cio_sha1_batch_dev: launch");
     e = hipStreamSynchronize(s);
     (void) hipFree(d);
     if (rc != CIO_OK) {

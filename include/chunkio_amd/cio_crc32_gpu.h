@@ -166,10 +166,14 @@ int  cio_crc32_batch_fd_multi(const int *fds, const uint64_t *foffs, const size_
 int  cio_crc32_host_register(const void *p, size_t len);
 int  cio_crc32_host_unregister(const void *p);
 
-/* Host-side legs of the last host/file batch that finished (any thread; per
- * device entry for *_multi): out[0..5] = total ms, copy into pinned staging
- * ms (caller thread's share of the pool's wall time), slot waits ms, plan
- * builds ms, staging groups, staged bytes.  Fills min(n, 6) values. */
+/* Host-side legs of a host/file batch: the calling thread's own last
+ * single-device batch (cio_crc32_batch_host, or a *_multi call with one
+ * device); if this thread has run none (e.g. it only made *_multi calls over
+ * several devices, which run on internal threads), the last device pipeline
+ * of any thread to finish -- last writer wins.  out[0..5] = total ms, copy
+ * into pinned staging ms (the caller's wall time over the copy, DMA issue
+ * included), slot waits ms, plan builds ms, staging groups, staged bytes.
+ * Fills min(n, 6) values. */
 int  cio_gpu_pipe_last_timing(double *out, int n);
 
 /* ---- batched CRC-32 on the host CPU ------------------------------------ */
