@@ -564,6 +564,7 @@ def run_e2e(args, rank, world, device, dist):
     import chunkio_amd as cio
     from chunkio_amd import workloads as wl
     lens, ids, seed, desc, scaling = geometry("e2e", rank, world)
+    bound = bind_to_gpu_node(device.index or 0)
     host, offs = wl.host_batch(seed, lens, align=16)
     for _ in range(max(1, args.warmup)):
         out = cio.crc32_batch_host_packed(host, offs, lens)
@@ -621,6 +622,7 @@ def run_e2e(args, rank, world, device, dist):
                                     "note": "host batch pinned once with cio_crc32_host_register "
                                             "(outside the timed loop); chunks DMA'd directly"},
             "host_cpu_batch": host_cpu,
+            "numa": {**numa_info(device.index or 0, host), "bound_cpus": bound},
             "breakdown": e2e_breakdown(host, device),
             "pipe_legs_last_call": {"staged": legs_staged, "registered": legs_reg,
                                     "note": "cio_gpu_pipe_last_timing() after the last timed call: total = the "
@@ -630,6 +632,63 @@ def run_e2e(args, rank, world, device, dist):
                                             "total minus the DMA bound (bytes / pinned_h2d_GBps) is "
                                             "pipeline fill/drain and host overhead"},
             "check": check}
+
+
+def page_node(addr):
+    """NUMA node of the page at addr (get_mempolicy MPOL_F_NODE|MPOL_F_ADDR), or -1."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        node = ctypes.c_int(-1)
+        rc = libc.syscall(239, ctypes.byref(node), None, ctypes.c_ulong(0), ctypes.c_void_p(addr),
+                          ctypes.c_ulong(3))
+        return node.value if rc == 0 else -1
+    except (OSError, AttributeError):
+        return -1
+
+
+def numa_info(dev_index, host=None):
+    """Where the host legs run: the GPU's NUMA node, the nodes of the host
+    batch's first and middle pages, and the CPUs this process may use."""
+    import chunkio_amd as cio
+    info = {"gpu_node": int(cio.lib().cio_gpu_numa_node(dev_index))}
+    try:
+        with open("/sys/devices/system/node/online") as f:
+            info["nodes_online"] = f.read().strip()
+    except OSError:
+        pass
+    if host is not None:
+        info["host_batch_nodes"] = [page_node(host.ctypes.data), page_node(host.ctypes.data + host.size // 2)]
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    return info
+
+
+def bind_to_gpu_node(dev_index):
+    """CIO_BENCH_NUMA_BIND=1: restrict this process to the GPU's NUMA node
+    before the host batch is allocated (as a deployment binds each rank to
+    its GPU's socket).  Returns the CPUs bound, or None."""
+    if os.environ.get("CIO_BENCH_NUMA_BIND") != "1":
+        return None
+    import chunkio_amd as cio
+    node = int(cio.lib().cio_gpu_numa_node(dev_index))
+    if node < 0:
+        return None
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = set()
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+            return len(cpus)
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def host_cpu_threads():
@@ -1118,7 +1177,7 @@ def other_configs(args, rank, world, device, dist):
         keep = {k: r[k] for k in ("metric", "value", "unit", "scaling", "steps", "warmup", "ms_per_step")}
         keep["workload"] = r["config"].get("workload")
         for k in ("roofline", "check", "per_gpu", "registered_in_place", "breakdown", "pipe_legs_last_call",
-                  "host_cpu_batch", "host_route", "host_paths",
+                  "host_cpu_batch", "host_route", "host_paths", "numa",
                   "cpu_baseline", "cpu_baseline_ref", "vs_baseline", "vs_baseline_note"):
             if k in r:
                 keep[k] = r[k]

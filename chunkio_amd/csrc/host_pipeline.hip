@@ -30,6 +30,9 @@ using namespace cioa;
 // device, so a chunk split over several groups chains its state on the GPU.
 
 #include <atomic>
+#include <ctype.h>
+#include <pthread.h>
+#include <sched.h>
 #include <thread>
 #include <condition_variable>
 #include <errno.h>
@@ -73,29 +76,6 @@ static size_t first_stage_bytes()
     }();
     return v;
 }
-// Streamed staging (default): a group's host copy is cut into sub-blocks of
-// CIO_GPU_DMA_SUB_MB MiB (default 4; 0 = one DMA per group after its whole
-// copy, the round-3 pipeline), and each sub-block's H2D DMA is queued as soon
-// as its bytes are in pinned memory.  The host copy (~63 GB/s with a DMA in
-// flight) outruns the link (~57 GB/s), so the DMA engine starts one
-// sub-block after the call begins and then never waits for a copy; groups
-// need not start small (they are all kStage) and no group's copy sits
-// between two DMAs.
-static size_t dma_sub_bytes()
-{
-    static const size_t v = [] {
-        long mb = 4;
-        if (const char *r = getenv("CIO_GPU_DMA_SUB_MB")) {
-            mb = atol(r);
-            if (mb < 0 || mb > 1024) {
-                mb = 4;
-            }
-        }
-        return (size_t) mb << 20;
-    }();
-    return v;
-}
-
 #ifdef CIO_PIPE_SLOTS
 constexpr int kSlots = CIO_PIPE_SLOTS;   // A/B builds only
 #else
@@ -123,6 +103,70 @@ struct HostGroup {
 // 4 MiB group in 1 MiB pieces kept 12 of the 16 threads idle while the DMA
 // engine waited for it).  The caller first runs `before` (the group's plan
 // build), overlapping it with the workers' copying.
+// CPUs of the NUMA node whose PCIe root the device hangs off, within this
+// process's affinity (empty when unknown: no sysfs node, node -1, or no
+// overlap).  *node_out = that node or -1.
+std::vector<int> device_local_cpus(int dev, int *node_out)
+{
+    *node_out = -1;
+    char bdf[64] = {0};
+    if (hipDeviceGetPCIBusId(bdf, (int) sizeof(bdf) - 1, dev) != hipSuccess) {
+        return {};
+    }
+    for (char *c = bdf; *c; ++c) {
+        *c = (char) tolower((unsigned char) *c);
+    }
+    char path[192];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bdf);
+    int node = -1;
+    if (FILE *f = fopen(path, "r")) {
+        if (fscanf(f, "%d", &node) != 1) {
+            node = -1;
+        }
+        fclose(f);
+    }
+    if (node < 0) {
+        return {};
+    }
+    *node_out = node;
+    snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+    std::vector<int> cpus;
+    if (FILE *f = fopen(path, "r")) {
+        int a, b;
+        char sep;
+        while (fscanf(f, "%d", &a) == 1) {
+            b = a;
+            if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+                if (fscanf(f, "%d", &b) != 1) {
+                    break;
+                }
+                if (fscanf(f, "%c", &sep) != 1) {
+                    sep = '\n';
+                }
+            }
+            for (int c = a; c <= b; c++) {
+                cpus.push_back(c);
+            }
+            if (sep != ',') {
+                break;
+            }
+        }
+        fclose(f);
+    }
+    cpu_set_t mine;
+    CPU_ZERO(&mine);
+    if (sched_getaffinity(0, sizeof(mine), &mine) != 0) {
+        return {};
+    }
+    std::vector<int> out;
+    for (int c : cpus) {
+        if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &mine)) {
+            out.push_back(c);
+        }
+    }
+    return out;
+}
+
 class CopyPool {
 public:
     static constexpr uint64_t kPieceMax = 1ull << 20;
@@ -142,12 +186,30 @@ public:
         return std::min(kPieceMax, std::max(kPieceMin, (per + kPieceMin - 1) & ~(kPieceMin - 1)));
     }
 
-    CopyPool()
+    // Workers run on the CPUs of the device's NUMA node when that is known
+    // (CIO_GPU_COPY_NUMA=0: wherever the scheduler puts them): the staging
+    // copy writes pinned memory the device DMAs from, and a copy thread on
+    // the far socket sends every byte over the inter-socket link first.
+    explicit CopyPool(int dev)
     {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned nw = std::min(15u, hw > 1 ? hw - 1 : 0u);
+        static const bool numa = [] {
+            const char *r = getenv("CIO_GPU_COPY_NUMA");
+            return !(r && r[0] == '0');
+        }();
+        int node = -1;
+        const std::vector<int> local = numa ? device_local_cpus(dev, &node) : std::vector<int>();
         for (unsigned t = 0; t < nw; t++) {
             workers_.emplace_back([this]() { run(); });
+            if (!local.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                for (int c : local) {
+                    CPU_SET(c, &set);
+                }
+                (void) pthread_setaffinity_np(workers_.back().native_handle(), sizeof(set), &set);
+            }
         }
     }
     ~CopyPool()
@@ -193,60 +255,6 @@ public:
         return ok && !failed_;
     }
 
-    // Streamed form: the group's bytes in sub-blocks of `sub` bytes (a
-    // multiple of the piece size).  The workers copy pieces in order; the
-    // caller runs `before`, then `issue(lo, hi)` for each sub-block in order
-    // as soon as every piece of it is in dst (the DMA of a sub-block starts
-    // while later ones are still being copied).  With no workers the caller
-    // copies and issues alone.
-    template <typename F, typename I>
-    bool copy_streamed(uint8_t *dst, const HostGroup &g, uint64_t sub, F before, I issue)
-    {
-        const uint64_t piece = std::min<uint64_t>(sub / 16 ? sub / 16 : sub, kPieceMax);
-        const uint64_t nsub = (g.bytes + sub - 1) / sub;
-        const uint64_t npieces = (g.bytes + piece - 1) / piece;
-        if (workers_.empty() || npieces <= 1) {
-            before();
-            const bool ok = range(dst, g, 0, g.bytes);
-            cioa_stage_fence();
-            for (uint64_t k = 0; k < nsub; k++) {
-                issue(k * sub, std::min<uint64_t>(g.bytes, (k + 1) * sub));
-            }
-            return ok;
-        }
-        const uint64_t per_sub = sub / piece;
-        sub_left_.reset(new std::atomic<uint32_t>[nsub]);
-        for (uint64_t k = 0; k < nsub; k++) {
-            const uint64_t lo = k * per_sub, hi = std::min(npieces, (k + 1) * per_sub);
-            sub_left_[k].store((uint32_t) (hi - lo), std::memory_order_relaxed);
-        }
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            dst_ = dst;
-            g_ = &g;
-            npieces_ = npieces;
-            piece_ = piece;
-            per_sub_ = per_sub;
-            next_.store(0, std::memory_order_relaxed);
-            pending_ = workers_.size();
-            failed_ = false;
-            ++gen_;
-        }
-        cv_.notify_all();
-        before();
-        for (uint64_t k = 0; k < nsub; k++) {
-            // the workers finish sub-blocks at ~4 MiB / 60 GB/s = ~70 us each
-            while (sub_left_[k].load(std::memory_order_acquire) != 0) {
-                __builtin_ia32_pause();
-            }
-            issue(k * sub, std::min<uint64_t>(g.bytes, (k + 1) * sub));
-        }
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return pending_ == 0; });
-        per_sub_ = 0;
-        return !failed_;
-    }
-
 private:
     bool drain(uint8_t *dst, const HostGroup &g, uint64_t npieces, uint64_t piece)
     {
@@ -257,11 +265,6 @@ private:
                 return ok;
             }
             ok &= range(dst, g, p * piece, std::min<uint64_t>(g.bytes, (p + 1) * piece));
-            if (per_sub_) {
-                // publish the piece's streaming stores before its sub-block's count
-                cioa_stage_fence();
-                sub_left_[p / per_sub_].fetch_sub(1, std::memory_order_release);
-            }
         }
     }
     static constexpr uint64_t kBounce = 256u << 10;
@@ -351,8 +354,6 @@ private:
     uint64_t piece_ = kPieceMax;
     std::atomic<uint64_t> next_{0};
     size_t pending_ = 0;
-    uint64_t per_sub_ = 0;                               // pieces per sub-block (0: not streamed)
-    std::unique_ptr<std::atomic<uint32_t>[]> sub_left_;  // pieces still to copy per sub-block
 };
 
 size_t align256(size_t x)
@@ -449,7 +450,7 @@ void slot_free(PipeSlot &s)
     s = PipeSlot();
 }
 
-hipError_t pipe_init(HostPipe &hp)
+hipError_t pipe_init(HostPipe &hp, int dev)
 {
     hipError_t e = hipSuccess;
     for (int b = 0; b < kSlots && e == hipSuccess; b++) {
@@ -468,7 +469,7 @@ hipError_t pipe_init(HostPipe &hp)
         hp.ready = false;
         return e;
     }
-    hp.pool = new CopyPool();
+    hp.pool = new CopyPool(dev);
     hp.ready = true;
     return e;
 }
@@ -651,8 +652,7 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
     // first groups are smaller (first_stage_bytes(), doubling up to kStage):
     // the DMA engine starts after a short copy instead of a full slot's.
     std::vector<HostGroup> groups(1);
-    const uint64_t sub = dma_sub_bytes();
-    uint64_t cap = sub && !getenv("CIO_GPU_STAGE_FIRST_MB") ? kStage : std::min<uint64_t>(first_stage_bytes(), kStage);
+    uint64_t cap = std::min<uint64_t>(first_stage_bytes(), kStage);
     for (size_t i = 0; i < n; i++) {
         const uint8_t *p = fds ? nullptr : reinterpret_cast<const uint8_t *>(bufs[i]);
         uint64_t left = lens[i], done = 0;
@@ -690,7 +690,7 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
         HostPipe *hp;
         ~Release() { pipe_release(dev, hp); }
     } release{dev, hp};
-    if (!hp->ready && (e = pipe_init(*hp)) != hipSuccess) {
+    if (!hp->ready && (e = pipe_init(*hp, dev)) != hipSuccess) {
         return fail("cio_crc32_batch_host: pipeline setup", e);
     }
     std::vector<uint32_t> init(n);
@@ -746,38 +746,6 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
             // the metadata copy and the kernel on this stream).
             if ((e = dma_registered(g, s.dbuf, s.stream)) != hipSuccess) break;
             build();
-        } else if (sub) {
-            // staged, streamed: the plan is built while the copy workers fill
-            // the slot, then each sub-block's DMA is queued as soon as it is
-            // copied (the plan image goes first: it is ready before them)
-            const double tc = timing ? wall_s() : 0;
-            bool meta_sent = false;
-            hipError_t ed = hipSuccess;
-            const bool ok = hp->pool->copy_streamed(s.pinned, g, sub, build, [&](uint64_t lo, uint64_t hi) {
-                if (ed != hipSuccess || e != hipSuccess || err) {
-                    return;
-                }
-                if (!meta_sent) {
-                    ed = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream);
-                    meta_sent = true;
-                }
-                if (ed == hipSuccess) {
-                    ed = hipMemcpyAsync(s.dbuf + lo, s.pinned + lo, hi - lo, hipMemcpyHostToDevice, s.stream);
-                }
-            });
-            if (timing) {
-                t_copy += wall_s() - tc;
-            }
-            if (!ok) {
-                rc = fail("cio_crc32_batch: short read from a file source");
-                break;
-            }
-            if (e == hipSuccess) {
-                e = ed;
-            }
-            if (e == hipSuccess && !err && !meta_sent) {
-                e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream);
-            }
         } else {
             // staged: the plan is built while the copy workers fill the slot
             const double tc = timing ? wall_s() : 0;
@@ -794,10 +762,8 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
             rc = fail(err);
             break;
         }
-        if (direct || !sub) {
-            if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
-        }
-        if (!direct && !sub) {
+        if ((e = hipMemcpyAsync(s.meta_d, s.meta_h, meta_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
+        if (!direct) {
             if ((e = hipMemcpyAsync(s.dbuf, s.pinned, g.bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess) break;
         }
         if (prev && (e = hipStreamWaitEvent(s.stream, prev, 0)) != hipSuccess) break;   // chained states
@@ -1084,6 +1050,13 @@ extern "C" int cio_gpu_pipe_last_timing(double *out, int n)
         out[i] = v[i];
     }
     return CIO_OK;
+}
+
+extern "C" int cio_gpu_numa_node(int dev)
+{
+    int node = -1;
+    (void) device_local_cpus(dev, &node);
+    return node;
 }
 
 extern "C" int cio_gpu_device_count(void)

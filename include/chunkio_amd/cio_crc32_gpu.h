@@ -66,6 +66,11 @@ int cio_gpu_device_count(void);
 int cio_gpu_set_device(int dev);
 int cio_gpu_get_device(void);            /* -1 on error */
 
+/* NUMA node the device's PCIe link attaches to (sysfs), -1 if unknown.  The
+ * host pipeline's copy threads run on that node's CPUs; a caller that owns
+ * the chunk buffers does best to allocate them there too. */
+int cio_gpu_numa_node(int dev);
+
 /* Human-readable reason for the last CIO_ERROR on this thread ("" if none). */
 const char *cio_gpu_last_error(void);
 
