@@ -1036,6 +1036,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                 if (crc_step(use)) {
                     piece_end();
                 }
+                if (STAMPS && it == 0) {
+                    t_step1 = __builtin_amdgcn_s_memrealtime();
+                }
+                if (STAMPS && it == iters / 2) {
+                    t_mid = __builtin_amdgcn_s_memrealtime();
+                }
             };
             for (uint64_t it = 0; it < iters; it += 2) {
                 half(it, cur, nxt);
@@ -2144,6 +2150,9 @@ static StreamKernel select_kernel(int prio, bool stamps, bool uniform, bool ahea
 {
     if (ahead) {
         if (l64) {
+            if (stamps) {    // per-wave stamps of the shipped cfg2 kernel (tools/stamps.py)
+                return crc32_stream_kernel<true, 1, true, true, true>;
+            }
             return prio ? crc32_stream_kernel<false, 1, true, true, true>
                         : crc32_stream_kernel<false, 0, true, true, true>;
         }
@@ -2205,7 +2214,8 @@ int cioa::plan_exec_impl(const cio_crc32_plan *p, const void *dev_base, const ui
         }
         return CIO_OK;
     }
-    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0, p->ahead && !p->stamps, p->l64);
+    auto kern = select_kernel(p->prio, p->stamps != nullptr, p->unsteps != 0, p->ahead && (!p->stamps || p->l64),
+                              p->l64);
     hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint8_t *>(dev_base), p->S, p->ustride, p->ua0, p->uvlen,
                        p->W, p->unsteps, p->uh, p->n, p->desc, p->wstart, p->tiny,
