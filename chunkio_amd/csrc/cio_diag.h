@@ -1,0 +1,89 @@
+/*
+ * cio_diag.h -- every compile-time A/B and diagnostic switch of the kernels,
+ * in one place.  A product build (`make`) defines none of them, so the
+ * defaults below ARE the shipped kernels.  A/B builds override one with
+ * `make ablib VAR=name DEFS=-DX=v` (or ablib_sha1), which writes a separate
+ * library under chunkio_amd/lib/ab/ for tools/ab_lib.py / tools/gpu_ab.sh.
+ *
+ * "Diagnostic" switches compute WRONG results on purpose (they remove work
+ * to price it); they exist only to measure, never to ship.
+ */
+#ifndef CIO_DIAG_H
+#define CIO_DIAG_H
+
+/* ---- crc32_gpu.hip ------------------------------------------------------ */
+
+/* Diagnostic: lanes read 16 slice / 4 shift table replicas instead of 32 / 8
+ * (the 2-way bank conflicts of a two-workgroups-per-CU layout, priced at
+ * today's occupancy).  Correct results, slower kernel. */
+#ifndef CIO_DIAG_HALF_REPLICAS
+#define CIO_DIAG_HALF_REPLICAS 0
+#endif
+
+/* Diagnostic: the stream kernel computes on register data instead of HBM
+ * loads (compute-only time; wrong CRCs). */
+#ifndef CIO_ABLATE_LOADS
+#define CIO_ABLATE_LOADS 0
+#endif
+
+/* Diagnostic: skip the arrival/fold step of split chunks (prices the tail;
+ * wrong CRCs for split chunks). */
+#ifndef CIO_DIAG_NO_ARRIVAL
+#define CIO_DIAG_NO_ARRIVAL 0
+#endif
+
+/* Diagnostic: 1 = finished waves stay resident ~5 us before exiting, 2 = they
+ * wait for their workgroup (correct results). */
+#ifndef CIO_DIAG_TAIL
+#define CIO_DIAG_TAIL 0
+#endif
+
+/* A/B: chunks whose pieces all lie in one workgroup fold through LDS (1,
+ * shipped) or through the global arrival counters (0). */
+#ifndef CIO_LDS_FOLD
+#define CIO_LDS_FOLD 1
+#endif
+
+/* Small-chunk kernel.  A/B: chunks in flight per wave (1 shipped, 2).
+ * Diagnostic bit mask: 1 = no lane multiply, 2 = no LDS CRC (wrong CRCs). */
+#ifndef CIO_SMALL_SLOTS
+#define CIO_SMALL_SLOTS 1
+#endif
+#ifndef CIO_SMALL_EXP
+#define CIO_SMALL_EXP 0
+#endif
+
+/* ---- sha1_gpu.hip -------------------------------------------------------- */
+
+/* A/B: blocks handed over per barrier, schedule waves, chunks per workgroup
+ * of the wide geometry. */
+#ifndef CIO_SHA1_GROUP
+#define CIO_SHA1_GROUP 4
+#endif
+#ifndef CIO_SHA1_SCHED_WAVES
+#define CIO_SHA1_SCHED_WAVES 1
+#endif
+#ifndef CIO_SHA1_CHAINS
+#define CIO_SHA1_CHAINS 32
+#endif
+
+/* A/B: 1 drops the asm anchor that keeps each block's rounds ahead of the
+ * next block's row reads (correct results, slower). */
+#ifndef CIO_SHA1_NO_ANCHOR
+#define CIO_SHA1_NO_ANCHOR 0
+#endif
+
+/* Diagnostic: per-workgroup shader-clock records of the round loop, read back
+ * by cio_sha1_diag_clock (tools/sha1_clock.py).  Correct results. */
+#ifndef CIO_SHA1_CLOCK_DIAG
+#define CIO_SHA1_CLOCK_DIAG 0
+#endif
+
+/* ---- host_pipeline.hip ---------------------------------------------------- */
+
+/* A/B: staging slots per host pipeline. */
+#ifndef CIO_PIPE_SLOTS
+#define CIO_PIPE_SLOTS 3
+#endif
+
+#endif /* CIO_DIAG_H */

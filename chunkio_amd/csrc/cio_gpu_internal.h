@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "cio_diag.h"
 #include "crc32_host.h"
 #include "chunkio_amd/cio_crc32_gpu.h"
 

@@ -185,7 +185,7 @@ __device__ __forceinline__ uint64_t wave_start(uint64_t w, uint64_t S, uint64_t 
 // -- the tables a workgroup would hold in half the LDS (80 KiB, two
 // workgroups per CU) -- so every lookup group of 32 lanes takes the 2-way
 // bank conflicts such a layout has, at the current occupancy.
-#ifdef CIO_DIAG_HALF_REPLICAS
+#if CIO_DIAG_HALF_REPLICAS
 constexpr uint32_t kSliceRepMask = 15u, kShiftRepMask = 3u;
 #else
 constexpr uint32_t kSliceRepMask = 31u, kShiftRepMask = 7u;
@@ -367,7 +367,7 @@ __device__ __forceinline__ void load_step(StepRegs &r, const uint8_t *cbase, uin
     const uint64_t last = (vlen - 1) & ~15ull;
 #pragma unroll
     for (int q = 0; q < kSub; ++q) {
-#ifdef CIO_ABLATE_LOADS
+#if CIO_ABLATE_LOADS
         // Diagnostic build only: compute without HBM (wrong CRCs).
         const uint64_t a = min(b0 + (uint64_t) q * kRow, last) + (uint64_t) (uintptr_t) cbase;
         r.q[q] = make_uint4((uint32_t) a, (uint32_t) (a >> 7) * 0x9E3779B9u, (uint32_t) a ^ 0x5bd1e995u,
@@ -664,16 +664,7 @@ __device__ __forceinline__ void rotate_prio(uint32_t slot_group, uint64_t it)
 // access.  The general path reads its WaveStart record first.  Separate
 // instantiations keep the general path's scalar-load wait out of the
 // uniform one's prologue.
-// Diagnostic builds only (make ablib DEFS=...): skip the arrival/fold step
-// (outputs of split chunks are then wrong) to price the kernel's tail.
-#ifndef CIO_DIAG_NO_ARRIVAL
-#define CIO_DIAG_NO_ARRIVAL 0
-#endif
-// Chunks whose pieces all lie in one workgroup are folded through LDS after
-// the stream (A/B knob: 0 = every split chunk takes the global arrival).
-#ifndef CIO_LDS_FOLD
-#define CIO_LDS_FOLD 1
-#endif
+// (CIO_DIAG_NO_ARRIVAL, CIO_LDS_FOLD, CIO_DIAG_TAIL: cio_diag.h.)
 // AHEAD (uniform batches of whole 4 KiB steps with no alignment head: every
 // step is full, so the partial-step paths compile out): two ring slots, and
 // the next step's loads are issued as soon as this step's data has landed,
@@ -1147,14 +1138,14 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             }
         }
     }
-#if defined(CIO_DIAG_TAIL) && CIO_DIAG_TAIL == 1
+#if CIO_DIAG_TAIL == 1
     {   // diagnostic: finished waves stay resident ~5 us (sleeping) before exiting
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < 500) {
             __builtin_amdgcn_s_sleep(10);
         }
     }
-#elif defined(CIO_DIAG_TAIL) && CIO_DIAG_TAIL == 2
+#elif CIO_DIAG_TAIL == 2
     __syncthreads();   // diagnostic: finished waves wait for the workgroup before exiting
 #endif
     if (STAMPS && lane == 0) {
@@ -1199,12 +1190,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
 // ring refill is the same loads (4 data rows; the un-shift factor unless the
 // batch is uniform; the seed when seeds are given), so the compiler's vmcnt
 // waits are exact.
-#ifndef SMALL_EXP
-#define SMALL_EXP 0
-#endif
-#ifndef SMALL_SLOTS
-#define SMALL_SLOTS 1            // chunks in flight per wave (A/B knob)
-#endif
+// (CIO_SMALL_SLOTS, CIO_SMALL_EXP: cio_diag.h.)
 struct SmallRegs {
     uint4 q[kSub];
     uint32_t inv;    // x^(-8 D), D = 4096 - virtual length
@@ -1297,7 +1283,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         }
     };
 
-#if SMALL_SLOTS == 2
+#if CIO_SMALL_SLOTS == 2
     SmallRegs ra, rb;
     issue(ra, c0);
     issue(rb, c0 + 1);
@@ -1388,7 +1374,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
                                        vlen);
                 }
             }
-            if (SMALL_EXP & 2) {
+            if (CIO_SMALL_EXP & 2) {
 #pragma unroll
                 for (int q = 0; q < kSub; ++q) {
                     st ^= r.q[q].x ^ r.q[q].y ^ r.q[q].z ^ r.q[q].w;
@@ -1408,10 +1394,10 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
             asm volatile("v_mov_b32 %0, %1" : "=v"(inv) : "v"(cur.inv));
         }
         // The next chunk's loads go out before the fold.
-        issue(cur, c + SMALL_SLOTS);
+        issue(cur, c + CIO_SMALL_SLOTS);
         if (live) {
             uint32_t x = st;
-            if (!(SMALL_EXP & 1)) {
+            if (!(CIO_SMALL_EXP & 1)) {
                 // 32 x (bit-field sign extend, fused and-xor)
                 x = col[0] & (0u - (st & 1u));
 #pragma unroll
@@ -1429,7 +1415,7 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
             }
         }
     };
-#if SMALL_SLOTS == 2
+#if CIO_SMALL_SLOTS == 2
     for (uint32_t c = c0; c < c1; c += 2) {
         chunk(ra, c);
         chunk(rb, c + 1);

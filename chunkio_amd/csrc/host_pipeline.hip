@@ -76,11 +76,7 @@ static size_t first_stage_bytes()
     }();
     return v;
 }
-#ifdef CIO_PIPE_SLOTS
-constexpr int kSlots = CIO_PIPE_SLOTS;   // A/B builds only
-#else
-constexpr int kSlots = 3;
-#endif
+constexpr int kSlots = CIO_PIPE_SLOTS;   // 3 (cio_diag.h)
 
 // One staging group.  A source is host memory (src[k]) or, for batches read
 // straight from files, a file range (fd[k], foff[k]) that the copy threads

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <stdlib.h>
 
+#include "cio_diag.h"
 #include "crc32_host.h"
 #include "chunkio_amd/cio_crc32_gpu.h"
 
@@ -178,21 +179,9 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
 // reads' latency is hidden; what they still cost (~6% of the chain) is
 // their issue and register-file writes.  Blocks are handed over kShaPer (4)
 // at a time through 2 kShaPer LDS slots, one barrier per group (~0.4%).
-#ifdef CIO_SHA1_GROUP
-constexpr int kShaPer = CIO_SHA1_GROUP;           // blocks handed over per barrier
-#else
-constexpr int kShaPer = 4;
-#endif
-#ifdef CIO_SHA1_SCHED_WAVES
-constexpr int kShaSched = CIO_SHA1_SCHED_WAVES;   // schedule waves
-#else
-constexpr int kShaSched = 1;
-#endif
-#ifdef CIO_SHA1_CHAINS
-constexpr int kShaChains = CIO_SHA1_CHAINS;       // chunks per workgroup (64, 32, 16 or 8)
-#else
-constexpr int kShaChains = 32;
-#endif
+constexpr int kShaPer = CIO_SHA1_GROUP;           // blocks handed over per barrier (4; cio_diag.h)
+constexpr int kShaSched = CIO_SHA1_SCHED_WAVES;   // schedule waves (1)
+constexpr int kShaChains = CIO_SHA1_CHAINS;       // chunks per workgroup, wide geometry (32)
 constexpr int kShaRowsPerBlock = 20;              // 80 rounds as 20 rows of 4 (ds_read/write_b128)
 constexpr int kShaAhead = 4;                      // own blocks in flight per schedule lane
 constexpr int kShaThreads = 64 * (1 + kShaSched);
@@ -224,7 +213,7 @@ using ShaGeomWide = ShaGeom<kShaChains, kShaPer>;   // the default (CIO_SHA1_CHA
 using ShaGeom16 = ShaGeom<16, 8>;
 using ShaGeom8 = ShaGeom<8, 8>;
 
-#ifdef CIO_SHA1_CLOCK_DIAG
+#if CIO_SHA1_CLOCK_DIAG
 // Diagnostic builds only: per workgroup, the round wave's shader-clock and
 // 100 MHz counters at the start and the end of its block loop (read back by
 // cio_sha1_diag_clock; tools/sha1_clock.py turns them into the clock the
@@ -403,7 +392,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
 #pragma unroll
         for (int u = 0; u < kShaPer; ++u) {
             const uint64_t jb = g * kShaPer + u;
-#ifndef CIO_SHA1_NO_ANCHOR
+#if !CIO_SHA1_NO_ANCHOR
             // The rounds are pure arithmetic, so the instruction selector may
             // move a block's rounds past the next block's reads (it did in the
             // select-free groups: blocks 3 and 0 then waited on reads issued
@@ -425,7 +414,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         }
     };
     __syncthreads();
-#ifdef CIO_SHA1_CLOCK_DIAG
+#if CIO_SHA1_CLOCK_DIAG
     const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -438,7 +427,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     for (; g < ngroups; ++g) {
         run_group(std::false_type(), g);
     }
-#ifdef CIO_SHA1_CLOCK_DIAG
+#if CIO_SHA1_CLOCK_DIAG
     {
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
         const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -619,7 +608,7 @@ int sha1_launch(const void *dev_base, const uint64_t *dev_offs, const uint64_t *
 
 }  // namespace
 
-#ifdef CIO_SHA1_CLOCK_DIAG
+#if CIO_SHA1_CLOCK_DIAG
 // Diagnostic builds only: copy the first nwg workgroups' clock records
 // (4 x u64 each: shader clock start/end, 100 MHz start/end) to host memory.
 extern "C" int cio_sha1_diag_clock(unsigned long long *out, int nwg)
