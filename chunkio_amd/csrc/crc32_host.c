@@ -47,6 +47,7 @@ const uint32_t *cioa_byte_table(void)
 }
 
 static uint32_t crc_update_table(uint32_t c, const unsigned char *p, size_t len);
+static uint32_t multmodp_bits(uint32_t a, uint32_t b);
 
 /* ---- carry-less multiply folding (x86 PCLMULQDQ / VPCLMULQDQ) -------------
  *
@@ -75,9 +76,9 @@ static uint32_t xpow_bits(uint64_t n)
     uint32_t r = 0x80000000u, sq = 0x40000000u;   /* x^0, x^1 */
     while (n) {
         if (n & 1u) {
-            r = cioa_multmodp(sq, r);
+            r = multmodp_bits(sq, r);
         }
-        sq = cioa_multmodp(sq, sq);
+        sq = multmodp_bits(sq, sq);
         n >>= 1;
     }
     return r;
@@ -252,7 +253,7 @@ static uint32_t crc_update_table(uint32_t c, const unsigned char *p, size_t len)
 }
 
 /* a(x)*b(x) mod P(x); bit 31 carries the x^0 coefficient (reflected). */
-uint32_t cioa_multmodp(uint32_t a, uint32_t b)
+static uint32_t multmodp_bits(uint32_t a, uint32_t b)
 {
     uint32_t p = 0;
     for (int i = 31; i >= 0; i--) {
@@ -260,6 +261,45 @@ uint32_t cioa_multmodp(uint32_t a, uint32_t b)
         b = (b >> 1) ^ (CIOA_POLY & (0u - (b & 1u)));
     }
     return p;
+}
+
+#if defined(__x86_64__)
+/* a * b mod P with one carry-less multiply.  In the reflected form bit k of a
+ * 32-bit word is x^(31-k), so the 63-bit product P = clmul(a, b) has bit k <->
+ * x^(62-k).  Its bits 31..62 (x^31..x^0) are already reduced and land at
+ * bits 0..31 of P >> 31.  Its bits 0..30 (x^62..x^32) are v(x) x^32 for the
+ * 32-bit message v = P << 1 (bit j <-> x^(31-j) of the message), i.e. the
+ * CRC of v's four bytes from state 0: four slice-table lookups. */
+static int mm_clmul;
+static pthread_once_t mm_once = PTHREAD_ONCE_INIT;
+
+static void build_mm(void)
+{
+    pthread_once(&s16_once, build_s16);
+    __builtin_cpu_init();
+    mm_clmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+}
+
+__attribute__((target("pclmul,sse4.1")))
+static uint32_t multmodp_clmul(uint32_t a, uint32_t b)
+{
+    const __m128i p = _mm_clmulepi64_si128(_mm_cvtsi32_si128((int) a), _mm_cvtsi32_si128((int) b), 0x00);
+    const uint64_t q = (uint64_t) _mm_cvtsi128_si64(p);
+    const uint32_t h = (uint32_t) (q >> 31);
+    const uint32_t v = (uint32_t) (q << 1);
+    return h ^ s16[3][v & 0xffu] ^ s16[2][(v >> 8) & 0xffu] ^ s16[1][(v >> 16) & 0xffu] ^ s16[0][v >> 24];
+}
+#endif
+
+uint32_t cioa_multmodp(uint32_t a, uint32_t b)
+{
+#if defined(__x86_64__)
+    pthread_once(&mm_once, build_mm);
+    if (mm_clmul) {
+        return multmodp_clmul(a, b);
+    }
+#endif
+    return multmodp_bits(a, b);
 }
 
 /* x^(8n) mod P by square-and-multiply over the bits of n. */
