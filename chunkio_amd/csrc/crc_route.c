@@ -25,7 +25,8 @@
  * so the host wins below B* = kGpuFixedUs / (1/r_host - 1/r_gpu), and for
  * every size once r_host >= r_gpu.  With chunkio's one thread (T = 1, the
  * default: the reference is single-threaded and so is Fluent Bit's caller)
- * B* is ~4 MiB per device.  With T >= 2 host threads the host's DRAM rate
+ * B* is ~86 MB per device (measured: one thread wins up to 128 x 400 KB,
+ * the GPU from 256 x 400 KB).  With T >= 2 host threads the host's DRAM rate
  * already beats one PCIe link, so host-resident batches stay on the CPU: the
  * GPU path pays off for host-resident chunks only when the caller cannot
  * spare cores.  CIOA_CPU_CRC_MAX / cio_crc32_set_cpu_max() override the
@@ -43,11 +44,14 @@
 #include "chunkio_amd/cio_crc32_gpu.h"
 #include "crc32_host.h"
 
-/* Cost-model rates (see the header comment). */
-static const double kGpuFixedUs = 85.0;      /* one-chunk GPU host batch at <= 4 KiB (crossover_r03b.txt) */
-static const double kGpuGBps = 47.0;         /* pipelined GPU host batch per device (bench e2e, staged) */
-static const double kCpuThreadGBps = 25.0;   /* crc_update, one thread, DRAM-resident */
-static const double kCpuMemGBps = 200.0;     /* host threads together, DRAM-resident */
+/* Cost-model rates (see the header comment), measured on the MI355X box by
+ * tools/route_batch.py (profiles/r04/route_batch_r04a.json: batches of 1..1024
+ * x 400 KB in DRAM-resident pageable memory): the GPU host batch's least-
+ * squares fixed cost and rate, crc_update's rate on one thread and on 16. */
+static const double kGpuFixedUs = 221.0;
+static const double kGpuGBps = 54.2;
+static const double kCpuThreadGBps = 47.6;
+static const double kCpuMemGBps = 396.0;
 
 static size_t g_cpu_max;
 static int g_cpu_max_set;

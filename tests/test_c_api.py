@@ -66,11 +66,14 @@ def test_chunk_api_reference_tests_immediate_and_deferred(cuda, tmp_path):
         assert rc == 0, out
 
 
-def test_chunk_api_reference_tests_host_route(tmp_path):
+@pytest.mark.parametrize("threads", ["1", "8"])
+def test_chunk_api_reference_tests_host_route(tmp_path, threads):
     """The same C replay with every chunk-layer CRC on the library's host
-    crc_update (CIOA_CPU_CRC_MAX huge, crc_route.c): the chunk API's
+    crc_update (CIOA_CPU_CRC_MAX huge, crc_route.c), on the calling thread and
+    on the 8-thread host pool (CIOA_HOST_CRC_THREADS): the chunk API's
     semantics do not depend on where the CRC runs.  (The deferred run
     compares its identity corpus with the immediate run's files.)"""
     for mode in ("immediate", "deferred"):
-        rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), mode], env={"CIOA_CPU_CRC_MAX": str(1 << 62)})
+        rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), mode],
+                       env={"CIOA_CPU_CRC_MAX": str(1 << 62), "CIOA_HOST_CRC_THREADS": threads})
         assert rc == 0 and "0 failed" in out, out

@@ -21,21 +21,24 @@ INIT = 0xFFFFFFFF
 # (cio_crc32_set_cpu_max(0)); the default in between is the measured
 # crossover.  Each chunk-layer test runs both ways: the host route in the CPU
 # suite, the GPU route under -m gpu.  Results must not depend on the route.
-ROUTES = [pytest.param("host", id="host"), pytest.param("gpu", marks=pytest.mark.gpu, id="gpu")]
+# "host_mt" is the host route with 8 host CRC threads (cio_crc32_batch_cpu's
+# pool, crc_cpu_batch.c).
+ROUTES = [pytest.param("host", id="host"), pytest.param("host_mt", id="host_mt"),
+          pytest.param("gpu", marks=pytest.mark.gpu, id="gpu")]
 
 
 @pytest.fixture
 def route(request):
-    from chunkio_amd import _lib
-    lib = _lib.lib()
-    old = lib.cio_crc32_cpu_max()
+    import chunkio_amd as cio
     if request.param == "gpu":
         request.getfixturevalue("cuda")
-        lib.cio_crc32_set_cpu_max(0)
+        cio.route(reset=True, cpu_max=0)
+    elif request.param == "host_mt":
+        cio.route(reset=True, cpu_max=1 << 62, threads=8)
     else:
-        lib.cio_crc32_set_cpu_max(1 << 62)
+        cio.route(reset=True, cpu_max=1 << 62, threads=1)
     yield request.param
-    lib.cio_crc32_set_cpu_max(old)
+    cio.route(reset=True)
 
 
 def _gpu_error():
@@ -608,7 +611,6 @@ def test_scan_verify_failure_registers_down(tmp_path):
     from chunkio_amd import _lib
     lib = _lib.lib()
     _make_stream(tmp_path, 4, corrupt=(2,))
-    old = lib.cio_crc32_cpu_max()
     lib.cio_crc32_set_cpu_max(0)
     try:
         ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM | cf.CIO_DELETE_IRRECOVERABLE, devices=[99],
@@ -623,7 +625,7 @@ def test_scan_verify_failure_registers_down(tmp_path):
         assert [c.data_size for c in chunks if c.is_up()] == [3, 703, 2103]
         ctx.close()
     finally:
-        lib.cio_crc32_set_cpu_max(old)
+        lib.cio_crc32_route_reset()
 
 
 @pytest.mark.gpu
