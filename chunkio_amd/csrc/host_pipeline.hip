@@ -372,13 +372,68 @@ struct PipeSlot {
     bool busy = false;
 };
 
+// A built plan image (the bytes stage_plan copies into a slot's pinned
+// arena) and the geometry it was built for.  Batches of the same geometry
+// recur -- the chunk layer's syncs of equal-sized chunks, a scan of
+// equal-sized files, a benchmark's repeated batch -- and building a group's
+// plan (ChunkDesc / WaveStart / fold factors for 4096 waves, ~0.1 ms) then
+// costs more than copying its ~330 KB image.  The key is the whole geometry
+// (offsets, lengths, chunk ids, wave count), compared in full on a hit.
+struct PlanImage {
+    uint64_t hash = 0;
+    uint32_t W = 0;
+    std::vector<uint64_t> offs, lens;
+    std::vector<uint32_t> cid;
+    std::vector<uint8_t> image;
+    size_t o_desc = 0, o_ws = 0, o_tiny = 0, o_pfac = 0, o_cid = 0, npfac = 0;
+    uint64_t S = 0, bytes = 0;
+    uint32_t ntiny = 0;
+    uint64_t used = 0;               // LRU clock
+};
+
 struct HostPipe {
     bool ready = false;
     CopyPool *pool = nullptr;
     PipeSlot slot[kSlots];
     uint32_t *state = nullptr;       // running raw CRC per chunk of the call
     size_t state_cap = 0;
+    std::vector<PlanImage> plans;    // plan image cache (one pipeline = one caller at a time)
+    uint64_t plan_clock = 0;
 };
+
+// Plan image cache size per pipeline (CIO_GPU_PLAN_CACHE entries, default
+// 32, 0 = off); entries are ~330 KB for a 64 MiB group of 400 KB chunks.
+static size_t plan_cache_entries()
+{
+    static const size_t v = [] {
+        long k = 32;
+        if (const char *r = getenv("CIO_GPU_PLAN_CACHE")) {
+            k = atol(r);
+            if (k < 0 || k > 1024) {
+                k = 32;
+            }
+        }
+        return (size_t) k;
+    }();
+    return v;
+}
+
+static uint64_t geometry_hash(const HostGroup &g, uint32_t W)
+{
+    uint64_t h = 0xcbf29ce484222325ull ^ W;
+    auto mix = [&](uint64_t x) {
+        h ^= x;
+        h *= 0x100000001b3ull;
+        h ^= h >> 29;
+    };
+    mix(g.offs.size());
+    for (size_t i = 0; i < g.offs.size(); i++) {
+        mix(g.offs[i]);
+        mix(g.lens[i]);
+        mix(g.cid[i]);
+    }
+    return h;
+}
 
 // Pipelines are pooled per device: a call takes an idle one (or builds one,
 // up to CIO_GPU_PIPES_PER_DEV, default 4) and gives it back when done, so
@@ -511,46 +566,84 @@ hipError_t grow_meta(PipeSlot &s, size_t need)
 }
 
 // Build group g's plan into slot s (pinned image + device arenas) and return
-// a launchable plan view over the slot's device memory.
-hipError_t stage_plan(PipeSlot &s, const HostGroup &g, DeviceState *st, cio_crc32_plan &view,
+// a launchable plan view over the slot's device memory.  A geometry seen
+// before on this pipeline copies its cached image instead of rebuilding it.
+hipError_t stage_plan(HostPipe &hp, PipeSlot &s, const HostGroup &g, DeviceState *st, cio_crc32_plan &view,
                       uint32_t **d_cid, size_t *meta_bytes, const char **err)
 {
     const size_t n = g.offs.size();
     plan_init(&view, st, n);
-    PlanHost ph;
-    if ((*err = plan_build(ph, g.offs.data(), g.lens.data(), n, view.W)) != nullptr) {
-        return hipSuccess;
+    const size_t ncache = plan_cache_entries();
+    const uint64_t h = ncache ? geometry_hash(g, view.W) : 0;
+    PlanImage *hit = nullptr;
+    for (auto &pi : hp.plans) {
+        if (pi.hash == h && pi.W == view.W && pi.offs == g.offs && pi.lens == g.lens && pi.cid == g.cid) {
+            hit = &pi;
+            break;
+        }
     }
-    const size_t o_desc = 0;
-    const size_t o_ws = o_desc + align256(ph.desc.size() * sizeof(ChunkDesc));
-    const size_t o_tiny = o_ws + align256(ph.ws.size() * sizeof(WaveStart));
-    const size_t o_pfac = o_tiny + align256(std::max<size_t>(1, ph.tiny.size()) * sizeof(uint32_t));
-    const size_t o_cid = o_pfac + align256(ph.pfac.size() * sizeof(uint32_t));
-    const size_t total = o_cid + align256(n * sizeof(uint32_t));
+    PlanImage built;
+    if (!hit) {
+        PlanHost ph;
+        if ((*err = plan_build(ph, g.offs.data(), g.lens.data(), n, view.W)) != nullptr) {
+            return hipSuccess;
+        }
+        PlanImage &pi = built;
+        pi.o_desc = 0;
+        pi.o_ws = pi.o_desc + align256(ph.desc.size() * sizeof(ChunkDesc));
+        pi.o_tiny = pi.o_ws + align256(ph.ws.size() * sizeof(WaveStart));
+        pi.o_pfac = pi.o_tiny + align256(std::max<size_t>(1, ph.tiny.size()) * sizeof(uint32_t));
+        pi.o_cid = pi.o_pfac + align256(ph.pfac.size() * sizeof(uint32_t));
+        pi.npfac = ph.pfac.size();
+        pi.S = ph.S;
+        pi.bytes = ph.bytes;
+        pi.ntiny = (uint32_t) ph.tiny.size();
+        pi.image.assign(pi.o_cid + align256(n * sizeof(uint32_t)), 0);
+        memcpy(pi.image.data() + pi.o_desc, ph.desc.data(), ph.desc.size() * sizeof(ChunkDesc));
+        memcpy(pi.image.data() + pi.o_ws, ph.ws.data(), ph.ws.size() * sizeof(WaveStart));
+        if (!ph.tiny.empty()) {
+            memcpy(pi.image.data() + pi.o_tiny, ph.tiny.data(), ph.tiny.size() * sizeof(uint32_t));
+        }
+        memcpy(pi.image.data() + pi.o_pfac, ph.pfac.data(), ph.pfac.size() * sizeof(uint32_t));
+        memcpy(pi.image.data() + pi.o_cid, g.cid.data(), n * sizeof(uint32_t));
+        hit = &built;
+    }
+    const PlanImage &pi = *hit;
+    const size_t total = pi.image.size();
     hipError_t e = grow_meta(s, total);
-    if (e == hipSuccess) e = grow_dev(&s.partials, &s.part_cap, ph.pfac.size(), false, s.stream);
+    if (e == hipSuccess) e = grow_dev(&s.partials, &s.part_cap, pi.npfac, false, s.stream);
     if (e == hipSuccess) e = grow_dev(&s.counters, &s.cnt_cap, std::max<size_t>(1, n), true, s.stream);
     if (e != hipSuccess) {
         return e;
     }
-    memcpy(s.meta_h + o_desc, ph.desc.data(), ph.desc.size() * sizeof(ChunkDesc));
-    memcpy(s.meta_h + o_ws, ph.ws.data(), ph.ws.size() * sizeof(WaveStart));
-    if (!ph.tiny.empty()) {
-        memcpy(s.meta_h + o_tiny, ph.tiny.data(), ph.tiny.size() * sizeof(uint32_t));
-    }
-    memcpy(s.meta_h + o_pfac, ph.pfac.data(), ph.pfac.size() * sizeof(uint32_t));
-    memcpy(s.meta_h + o_cid, g.cid.data(), n * sizeof(uint32_t));
-    view.S = ph.S;
-    view.bytes = ph.bytes;
-    view.ntiny = (uint32_t) ph.tiny.size();
-    view.desc = reinterpret_cast<ChunkDesc *>(s.meta_d + o_desc);
-    view.wstart = reinterpret_cast<WaveStart *>(s.meta_d + o_ws);
-    view.tiny = reinterpret_cast<uint32_t *>(s.meta_d + o_tiny);
-    view.pfac = reinterpret_cast<uint32_t *>(s.meta_d + o_pfac);
+    memcpy(s.meta_h, pi.image.data(), total);
+    view.S = pi.S;
+    view.bytes = pi.bytes;
+    view.ntiny = pi.ntiny;
+    view.desc = reinterpret_cast<ChunkDesc *>(s.meta_d + pi.o_desc);
+    view.wstart = reinterpret_cast<WaveStart *>(s.meta_d + pi.o_ws);
+    view.tiny = reinterpret_cast<uint32_t *>(s.meta_d + pi.o_tiny);
+    view.pfac = reinterpret_cast<uint32_t *>(s.meta_d + pi.o_pfac);
     view.partials = s.partials;
     view.counters = s.counters;
-    *d_cid = reinterpret_cast<uint32_t *>(s.meta_d + o_cid);
+    *d_cid = reinterpret_cast<uint32_t *>(s.meta_d + pi.o_cid);
     *meta_bytes = total;
+    hit->used = ++hp.plan_clock;
+    if (hit == &built && ncache) {
+        // keep it: evict the least recently used entry when full
+        built.hash = h;
+        built.W = view.W;
+        built.offs = g.offs;
+        built.lens = g.lens;
+        built.cid = g.cid;
+        if (hp.plans.size() < ncache) {
+            hp.plans.push_back(std::move(built));
+        } else {
+            auto lru = std::min_element(hp.plans.begin(), hp.plans.end(),
+                                        [](const PlanImage &a, const PlanImage &b) { return a.used < b.used; });
+            *lru = std::move(built);
+        }
+    }
     return hipSuccess;
 }
 
@@ -731,7 +824,7 @@ int batch_host_current(const void *const *bufs, const int *fds, const uint64_t *
         // the group's plan (host image into the slot's pinned arena)
         auto build = [&] {
             const double tp = timing ? wall_s() : 0;
-            e = stage_plan(s, g, st, view, &d_cid, &meta_bytes, &err);
+            e = stage_plan(*hp, s, g, st, view, &d_cid, &meta_bytes, &err);
             if (timing) {
                 t_plan += wall_s() - tp;
             }

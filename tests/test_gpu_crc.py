@@ -446,6 +446,27 @@ def test_host_batch_packed_and_graduated_groups(cuda):
 
 
 @pytest.mark.gpu
+def test_host_plan_cache_same_geometry_new_data(cuda):
+    """The host pipeline caches plan images by geometry (host_pipeline.hip
+    PlanImage): repeated calls of one geometry with different bytes and seeds,
+    interleaved with a geometry that differs in one length and one that
+    differs only in chunk order (a permutation: same offsets set, other
+    ids), must each give the oracle's CRCs."""
+    rng = np.random.default_rng(31)
+    lens = rng.integers(1, 2_000_000, 150).astype(np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    total = wl.batch_bytes(offs, lens) + 16
+    lens2 = lens.copy()
+    lens2[77] -= 1
+    perm = rng.permutation(len(lens))
+    for rep in range(3):
+        host = rng.integers(0, 256, total, dtype=np.uint8)
+        seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+        for o, ln in ((offs, lens), (offs, lens2), (offs[perm], lens[perm])):
+            want = po.crc_batch(host, o, ln, seeds=seeds)
+            np.testing.assert_array_equal(cio.crc32_batch_host_packed(host, o, ln, seeds=seeds), want)
+
+
 def test_host_pipeline_reuse_and_growth(cuda):
     """The persistent host pipeline across calls whose shapes grow and shrink
     (plan arenas reallocated, counters re-zeroed, state array regrown)."""
