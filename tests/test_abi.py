@@ -163,3 +163,36 @@ print(len(hip), hip[0].startswith("/opt/rocm"), _lib._hip_runtime is None)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["1", "True", "True"], r.stdout
+
+
+def test_hip_runtime_pin_checks_soname(tmp_path, monkeypatch):
+    """torch's libamdhip64 is pinned only when its SONAME is the one
+    libchunkio_amd.so links (DT_NEEDED); a mismatching file is left alone with
+    a warning naming both."""
+    from chunkio_amd import _lib
+    soname, _ = _lib._elf_dynamic_strings(_lib.LIB_PATH)
+    _, needed = _lib._elf_dynamic_strings(_lib.LIB_PATH)
+    assert any(x.startswith("libamdhip64.so") for x in needed), needed
+    assert _lib._elf_dynamic_strings(str(tmp_path / "missing.so")) == (None, [])
+    (tmp_path / "not_elf.so").write_bytes(b"not an elf file")
+    assert _lib._elf_dynamic_strings(str(tmp_path / "not_elf.so")) == (None, [])
+    # a torch whose runtime is another major version: no pin, a warning
+    real = _lib._elf_dynamic_strings
+
+    def fake(path):
+        if path.endswith("libamdhip64.so"):
+            return "libamdhip64.so.99", []
+        return real(path)
+    monkeypatch.setattr(_lib, "_elf_dynamic_strings", fake)
+    monkeypatch.delenv("CIOA_HIP_RUNTIME", raising=False)
+    import sys
+    had_torch = sys.modules.pop("torch", None)
+    try:
+        import importlib.util
+        if importlib.util.find_spec("torch") is None:
+            pytest.skip("torch not installed")
+        with pytest.warns(UserWarning, match="not pinning"):
+            assert _lib._pin_hip_runtime() is None
+    finally:
+        if had_torch is not None:
+            sys.modules["torch"] = had_torch
