@@ -34,8 +34,7 @@ constexpr uint32_t kSliceBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 
 constexpr uint32_t kShiftBytes = 32768;     // 4 tables x 256 x 8 replicas x 4 B
 constexpr uint32_t kShiftOff = kSliceBytes;
 constexpr uint32_t kLdsBytes = kSliceBytes + kShiftBytes;   // all 160 KiB of the CU
-constexpr int kStampWords = 12;
-              // diagnostic stamps per wave (CIO_GPU_STAMPS)
+constexpr int kStampWords = 16;             // diagnostic stamps per wave (CIO_GPU_STAMPS)
 
 struct ChunkDesc {
     uint64_t a;        // aligned-down start offset from the batch base

@@ -685,7 +685,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
     unsigned long long t_entry = 0, t_tables = 0, t_stream = 0, t_first = 0, t_mid = 0, t_issued = 0;
-    unsigned long long t_wt[2] = {0, 0}, t_step1 = 0;
+    unsigned long long t_wt[2] = {0, 0}, t_step1 = 0, t_arrived = 0, t_bar1 = 0, t_bar2 = 0, t_folded = 0;
     if (STAMPS) {
         t_entry = __builtin_amdgcn_s_memrealtime();
     }
@@ -1115,15 +1115,24 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         }
     }
 
+    if (STAMPS) {
+        t_arrived = __builtin_amdgcn_s_memrealtime();
+    }
     tiny_chunks(lds, lb_lo, base, desc, tiny, seeds, out, cid, ntiny, wave, lane, W);
     if (CIO_LDS_FOLD) {
         // Every wave is past its last table lookup: the LDS words are free.
         __syncthreads();
+        if (STAMPS) {
+            t_bar1 = __builtin_amdgcn_s_memrealtime();
+        }
         uint32_t *slot = reinterpret_cast<uint32_t *>(lds);
         if (lane == 0) {
             slot[tid >> 6] = pub;    // 0 unless the range ended inside a local chunk
         }
         __syncthreads();
+        if (STAMPS) {
+            t_bar2 = __builtin_amdgcn_s_memrealtime();
+        }
         if (wfl & kWfFold) {
             // Lane i < 16 <-> wave (wave - 16 + i); the nb waves before this
             // one hold the chunk's earlier pieces (empty ranges published 0).
@@ -1136,6 +1145,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             if (lane == 0) {
                 out[cid ? cid[c0] : c0] = a;
             }
+        }
+        if (STAMPS) {
+            t_folded = __builtin_amdgcn_s_memrealtime();
         }
     }
 #if CIO_DIAG_TAIL == 1
@@ -1165,6 +1177,10 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         stamps[kStampWords * wave + 9] = t_wt[0];    // table build: compact arrays written
         stamps[kStampWords * wave + 10] = t_wt[1];   // table build: gathered
         stamps[kStampWords * wave + 11] = t_step1;  // first step CRC'd
+        stamps[kStampWords * wave + 12] = t_arrived;  // after the arrival step
+        stamps[kStampWords * wave + 13] = t_bar1;     // LDS fold: past the first barrier
+        stamps[kStampWords * wave + 14] = t_bar2;     // LDS fold: past the second barrier
+        stamps[kStampWords * wave + 15] = t_folded;   // LDS fold done (output stored)
     }
 }
 

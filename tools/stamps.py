@@ -37,11 +37,13 @@ def main():
         for k in range(16):
             plan.exec(bufs[(it + k) % 4], out)
         torch.cuda.synchronize()
-        st = np.zeros(4096 * 12 * 2, np.uint64)
+        K = 16                    # kStampWords (cio_gpu_internal.h)
+        st = np.zeros(4096 * K * 2, np.uint64)
         W = f(plan._handle, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), st.size)
-        raw = st[:W * 12].reshape(W, 12).astype(np.int64)
-        # entry, tables, stream, exit, first, mid, loads issued, build phase 1, build phase 2
-        t = np.concatenate([raw[:, :4], raw[:, 6:12]], axis=1)
+        raw = st[:W * K].reshape(W, K).astype(np.int64)
+        # entry, tables, stream, exit, first, mid, loads issued, build phase 1, build phase 2, step 1,
+        # arrived, barrier 1, barrier 2, folded
+        t = np.concatenate([raw[:, :4], raw[:, 6:16]], axis=1)
         hw, xcc = raw[:, 4], raw[:, 5]
         simd = (hw >> 4) & 3
         print("   simd of wave slot (WG 0..3):", [list(simd.reshape(-1, 16)[b]) for b in range(4)])
@@ -64,6 +66,16 @@ def main():
         print("   exit       ", q(us[:, 3]))
         print("   stream dur ", q(us[:, 2] - us[:, 1]))
         print("   tail dur   ", q(us[:, 3] - us[:, 2]))
+        print("   arrived - stream done ", q(us[:, 10] - us[:, 2]))
+        print("   barrier1 - arrived    ", q(us[:, 11] - us[:, 10]))
+        print("   barrier2 - barrier1   ", q(us[:, 12] - us[:, 11]))
+        print("   folded - barrier2     ", q(us[:, 13] - us[:, 12]))
+        print("   exit - folded         ", q(us[:, 3] - us[:, 13]))
+        wgb1 = us[:, 11].reshape(-1, 16)
+        print("   WG barrier1 - WG max stream done", q(wgb1.max(1) - us[:, 2].reshape(-1, 16).max(1)))
+        lastw = int(np.argmax(us[:, 3]))
+        print("   last wave: stream %.2f arrived %.2f bar1 %.2f bar2 %.2f folded %.2f exit %.2f" %
+              tuple(us[lastw, k] for k in (2, 10, 11, 12, 13, 3)))
         ent = us[:, 0].reshape(-1, 16)
         tab = us[:, 1].reshape(-1, 16)
         print("   WG entry spread (last-first wave)", q(ent.max(1) - ent.min(1)))
