@@ -667,10 +667,12 @@ def numa_info(dev_index, host=None):
 
 
 def bind_to_gpu_node(dev_index):
-    """CIO_BENCH_NUMA_BIND=1: restrict this process to the GPU's NUMA node
-    before the host batch is allocated (as a deployment binds each rank to
-    its GPU's socket).  Returns the CPUs bound, or None."""
-    if os.environ.get("CIO_BENCH_NUMA_BIND") != "1":
+    """Restrict this process to the GPU's NUMA node before the host batch is
+    allocated, as a deployment binds each rank to its GPU's socket (the host
+    legs' pages and threads then sit next to the PCIe link they feed).
+    CIO_BENCH_NUMA_BIND=0 leaves the affinity alone.  Returns the number of
+    CPUs bound to, or None."""
+    if os.environ.get("CIO_BENCH_NUMA_BIND") == "0":
         return None
     import chunkio_amd as cio
     node = int(cio.lib().cio_gpu_numa_node(dev_index))
