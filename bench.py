@@ -261,6 +261,26 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
         res["multi_thread"] = {"value": round(float(lens_c.sum()) * mreps / secs_mt / 1e9, 3), "unit": "GB/s",
                                "threads": nt, "bit_exact_vs_gpu": bool(np.array_equal(out_mt, gpu_out)),
                                "sample": f"same batch x {mreps} passes, chunk i on thread i % {nt}"}
+    # The library's own host path over the same batch (crc_update with
+    # VPCLMULQDQ folding, cio_crc32_batch_cpu), 1 thread and the per-GPU CPU
+    # share: what a host-resident batch costs without the GPU.  Not the
+    # baseline (that is the reference's crc32.c above), reported beside it.
+    try:
+        import chunkio_amd as cio
+        lib_host = {}
+        for t in sorted({1, host_cpu_threads()}):
+            cio.crc32_batch_cpu_packed(host_buf, offs_c, lens_c, threads=t)
+            hreps = 8 if t == 1 else 32
+            t0 = time.perf_counter()
+            for _ in range(hreps):
+                got = cio.crc32_batch_cpu_packed(host_buf, offs_c, lens_c, threads=t)
+            dt = time.perf_counter() - t0
+            lib_host[f"threads_{t}"] = {"GBps": round(float(lens_c.sum()) * hreps / dt / 1e9, 2),
+                                        "bit_exact_vs_gpu": bool(np.array_equal(got, gpu_out))}
+        lib_host["sample"] = "same batch, cio_crc32_batch_cpu (the library's host crc_update), back-to-back passes"
+        res["library_host_path"] = lib_host
+    except Exception as e:  # informational
+        res["library_host_path"] = {"error": str(e)}
     # tools/cio -k -p restatement (BASELINE config 1), bounded sample of files.
     try:
         d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8)
