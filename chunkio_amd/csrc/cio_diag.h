@@ -44,6 +44,12 @@
 #define CIO_LDS_FOLD 1
 #endif
 
+/* A/B: the issue-ahead stream kernel peels each wave's last step off its
+ * loop so that step issues no refill (1), or refills unconditionally (0). */
+#ifndef CIO_AHEAD_PEEL
+#define CIO_AHEAD_PEEL 1
+#endif
+
 /* Small-chunk kernel.  A/B: chunks in flight per wave (1 shipped, 2).
  * Diagnostic bit mask: 1 = no lane multiply, 2 = no LDS CRC (wrong CRCs). */
 #ifndef CIO_SMALL_SLOTS

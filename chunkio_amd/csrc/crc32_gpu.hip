@@ -44,6 +44,8 @@
 #include <string>
 #include <algorithm>
 
+#include <type_traits>
+
 #include "cio_gpu_internal.h"
 
 using namespace cioa;
@@ -1013,7 +1015,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                                   "+v"(r.q[2].x), "+v"(r.q[2].y), "+v"(r.q[2].z), "+v"(r.q[2].w),
                                   "+v"(r.q[3].x), "+v"(r.q[3].y), "+v"(r.q[3].z), "+v"(r.q[3].w));
             };
-            auto half = [&](uint64_t it, StepRegs &use, StepRegs &fill) {
+            auto half = [&](uint64_t it, StepRegs &use, StepRegs &fill, auto refill) {
                 if (PRIO) {
                     rotate_prio(slot_group, it);
                 }
@@ -1023,7 +1025,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                     xlast = multmodp(wl, xl);
                 }
                 landed(use);
-                issue(fill);    // unconditional: one load sequence on every path
+                if (decltype(refill)::value) {
+                    issue(fill);    // unconditional in the loop: one load sequence on every path
+                }
                 if (crc_step(use)) {
                     piece_end();
                 }
@@ -1034,12 +1038,32 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                     t_mid = __builtin_amdgcn_s_memrealtime();
                 }
             };
+            using Refill = std::true_type;
+#if CIO_AHEAD_PEEL
+            // The wave's last step is peeled off the loop: it issues no
+            // refill, so the wave does not end waiting for four loads nobody
+            // reads (the refill past the range re-reads the slice table; its
+            // latency sat on every wave's tail, behind the vmcnt(0) below).
+            using NoRefill = std::false_type;
+            uint64_t it = 0;
+            for (; it + 2 < iters; it += 2) {
+                half(it, cur, nxt, Refill());
+                half(it + 1, nxt, cur, Refill());
+            }
+            if (iters - it == 2) {
+                half(it, cur, nxt, Refill());
+                half(it + 1, nxt, cur, NoRefill());
+            } else if (iters - it == 1) {
+                half(it, cur, nxt, NoRefill());
+            }
+#else
             for (uint64_t it = 0; it < iters; it += 2) {
-                half(it, cur, nxt);
+                half(it, cur, nxt, Refill());
                 if (it + 1 < iters) {
-                    half(it + 1, nxt, cur);
+                    half(it + 1, nxt, cur, Refill());
                 }
             }
+#endif
         }
         for (uint64_t it = 0; !AHEAD && it < iters; ++it) {
             if (PRIO) {
