@@ -25,8 +25,8 @@
  * so the host wins below B* = kGpuFixedUs / (1/r_host - 1/r_gpu), and for
  * every size once r_host >= r_gpu.  With chunkio's one thread (T = 1, the
  * default: the reference is single-threaded and so is Fluent Bit's caller)
- * B* is ~86 MB per device (measured: one thread wins up to 128 x 400 KB,
- * the GPU from 256 x 400 KB).  With T >= 2 host threads the host's DRAM rate
+ * B* is ~11 MB per device (measured crossovers: between 52 and 105 MB on
+ * the fast box, between 13 and 26 MB on the slow one).  With T >= 2 host threads the host's DRAM rate
  * already beats one PCIe link, so host-resident batches stay on the CPU: the
  * GPU path pays off for host-resident chunks only when the caller cannot
  * spare cores.  CIOA_CPU_CRC_MAX / cio_crc32_set_cpu_max() override the
@@ -44,14 +44,18 @@
 #include "chunkio_amd/cio_crc32_gpu.h"
 #include "crc32_host.h"
 
-/* Cost-model rates (see the header comment), measured on the MI355X box by
- * tools/route_batch.py (profiles/r04/route_batch_r04a.json: batches of 1..1024
- * x 400 KB in DRAM-resident pageable memory): the GPU host batch's least-
- * squares fixed cost and rate, crc_update's rate on one thread and on 16. */
-static const double kGpuFixedUs = 221.0;
-static const double kGpuGBps = 54.2;
-static const double kCpuThreadGBps = 47.6;
-static const double kCpuMemGBps = 396.0;
+/* Cost-model rates (see the header comment), measured on MI355X boxes by
+ * tools/route_batch.py (batches of 1..1024 x 400 KB in DRAM-resident
+ * pageable memory): the GPU host batch's least-squares fixed cost and rate
+ * (profiles/r04/route_batch_r04d.json: 163.5 us, 54.7 GB/s), and
+ * crc_update's rate on one thread and on 16, which differ by box (r04a:
+ * 47.6 / 396 GB/s; r04d: 27.4 / 131 GB/s).  The host rates are taken near
+ * the slower box, so an ambiguous batch goes to the GPU and leaves the
+ * host's cores to the caller. */
+static const double kGpuFixedUs = 163.5;
+static const double kGpuGBps = 54.7;
+static const double kCpuThreadGBps = 30.0;
+static const double kCpuMemGBps = 131.0;
 
 static size_t g_cpu_max;
 static int g_cpu_max_set;

@@ -205,7 +205,7 @@ int  cio_crc32_batch_fd_cpu(const int *fds, const uint64_t *foffs, const size_t 
  * batches on the GPU (cio_crc32_batch_host_multi / _fd_multi).  Same results
  * either way.  The default threshold is a cost model with rates measured on
  * the MI355X box (crc_route.c): with the default single host thread it is
- * ~86 MB per device in the call's device list; with two or more host threads
+ * ~11 MB per device in the call's device list; with two or more host threads
  * the host's DRAM rate beats a PCIe link and every host-memory batch stays on
  * the CPU.  CIOA_CPU_CRC_MAX (bytes) or cio_crc32_set_cpu_max() override the
  * threshold, 0 sends everything to the GPU; CIOA_HOST_CRC_THREADS or
