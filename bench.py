@@ -591,8 +591,11 @@ def run_e2e(args, rank, world, device, dist):
     barrier(dist)
     t0 = time.perf_counter()
     steps = max(1, min(args.steps, 30))
+    call_s = []
     for _ in range(steps):
+        tc = time.perf_counter()
         out = cio.crc32_batch_host_packed(host, offs, lens)
+        call_s.append(time.perf_counter() - tc)
     barrier(dist)
     elapsed = max_over_ranks(time.perf_counter() - t0, dist, device)
     value = int(lens.sum()) * world * steps / elapsed / 1e9
@@ -635,6 +638,8 @@ def run_e2e(args, rank, world, device, dist):
             "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
             "data": "synthetic, pageable host memory", "config": desc,
+            "staged_call_ms": {"min": round(min(call_s) * 1e3, 3), "median": round(float(np.median(call_s)) * 1e3, 3),
+                               "max": round(max(call_s) * 1e3, 3)},
             "registered_in_place": {"value": round(value_reg, 3), "unit": "GB/s",
                                     "ms_per_step": round(elapsed_reg / steps * 1e3, 4),
                                     "register_ms_once": round(reg_ms, 2),
@@ -1199,7 +1204,7 @@ def other_configs(args, rank, world, device, dist):
         keep = {k: r[k] for k in ("metric", "value", "unit", "scaling", "steps", "warmup", "ms_per_step")}
         keep["workload"] = r["config"].get("workload")
         for k in ("roofline", "check", "per_gpu", "registered_in_place", "breakdown", "pipe_legs_last_call",
-                  "host_cpu_batch", "host_route", "host_paths", "numa",
+                  "host_cpu_batch", "host_route", "host_paths", "numa", "staged_call_ms",
                   "cpu_baseline", "cpu_baseline_ref", "vs_baseline", "vs_baseline_note"):
             if k in r:
                 keep[k] = r[k]
