@@ -50,6 +50,12 @@
 #define CIO_AHEAD_PEEL 1
 #endif
 
+/* A/B: the stream kernel builds its LDS tables before (1) or after (0,
+ * shipped) requesting its first step's data. */
+#ifndef CIO_TABLES_FIRST
+#define CIO_TABLES_FIRST 0
+#endif
+
 /* Small-chunk kernel.  A/B: chunks in flight per wave (1 shipped, 2).
  * Diagnostic bit mask: 1 = no lane multiply, 2 = no LDS CRC (wrong CRCs). */
 #ifndef CIO_SMALL_SLOTS

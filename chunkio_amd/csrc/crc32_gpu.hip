@@ -785,6 +785,22 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         }
     };
 
+    // Table entries are computed, not loaded: at kernel start every global
+    // load pays cold-cache latency, and the build sits on the critical path.
+    auto build_tables = [&]() {
+        uint32_t tab_v[kE], tab_sv[kE];
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+            const uint32_t idx = tid + (uint32_t) kThreads * e;
+            table_entries<L64 ? cx_xpow8n(kStep - 64) : kXStepShift>(__builtin_amdgcn_readfirstlane(idx >> 8),
+                                                                     idx & 255u, tab_v[e], tab_sv[e]);
+        }
+        write_tables<STAMPS>(lds, tid, tab_v, tab_sv, t_wt);
+    };
+#if CIO_TABLES_FIRST
+    build_tables();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // The first step is requested before the table build so that its HBM
     // latency overlaps it (requesting two was slower: profiles/r01/ab_v4_steps.txt).
     // Unconditional (also for inactive waves): a branch here would merge a
@@ -837,16 +853,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         t_issued = __builtin_amdgcn_s_memrealtime();
     }
 
-    // Table entries are computed, not loaded: at kernel start every global
-    // load pays cold-cache latency, and the build sits on the critical path.
-    uint32_t tab_v[kE], tab_sv[kE];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-        const uint32_t idx = tid + (uint32_t) kThreads * e;
-        table_entries<L64 ? cx_xpow8n(kStep - 64) : kXStepShift>(__builtin_amdgcn_readfirstlane(idx >> 8),
-                                                                 idx & 255u, tab_v[e], tab_sv[e]);
-    }
-    write_tables<STAMPS>(lds, tid, tab_v, tab_sv, t_wt);
+#if !CIO_TABLES_FIRST
+    build_tables();
+#endif
     __syncthreads();
     if (STAMPS) {
         t_tables = __builtin_amdgcn_s_memrealtime();
