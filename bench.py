@@ -1185,6 +1185,10 @@ def other_configs(args, rank, world, device, dist):
         # verify-on-load of 1000 chunk files, and the config-1 loop through
         # the C chunk layer with deferred CRC + batched GPU sync.
         legs += [("verify", 3, 1), ("perf", 2, 1)]
+    if os.environ.get("CIO_BENCH_LEGS"):
+        # diagnostic: a subset / order of the legs (e.g. "e2e,cfg3")
+        by = {cfg: (cfg, s, w) for cfg, s, w in legs}
+        legs = [by[c] for c in os.environ["CIO_BENCH_LEGS"].split(",") if c in by]
     for cfg, steps, warm in legs:
         torch.cuda.empty_cache()
         a = copy.copy(args)
