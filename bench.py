@@ -585,9 +585,34 @@ def run_e2e(args, rank, world, device, dist):
     from chunkio_amd import workloads as wl
     lens, ids, seed, desc, scaling = geometry("e2e", rank, world)
     bound = bind_to_gpu_node(device.index or 0)
+    pre = []
+    if os.environ.get("CIO_BENCH_PRE_STREAMS"):
+        # diagnostic: streams that exist (and have run work) before the
+        # pipeline's own streams are created
+        import torch
+        for _ in range(int(os.environ["CIO_BENCH_PRE_STREAMS"])):
+            st_ = torch.cuda.Stream(device)
+            with torch.cuda.stream(st_):
+                torch.ones(16, device=device).sum()
+            pre.append(st_)
+        torch.cuda.synchronize(device)
+    def big_alloc():
+        # diagnostic: a large device allocation made, written and freed
+        import torch
+        big = torch.empty(int(float(os.environ["CIO_BENCH_PRE_ALLOC_GB"]) * 1e9), dtype=torch.uint8, device=device)
+        big.fill_(1)
+        torch.cuda.synchronize(device)
+        del big
+        torch.cuda.empty_cache()
+        time.sleep(float(os.environ.get("CIO_BENCH_ALLOC_SETTLE_S", "0")))
+    alloc_after = os.environ.get("CIO_BENCH_ALLOC_AFTER_WARM") == "1"
+    if os.environ.get("CIO_BENCH_PRE_ALLOC_GB") and not alloc_after:
+        big_alloc()
     host, offs = wl.host_batch(seed, lens, align=16)
     for _ in range(max(1, args.warmup)):
         out = cio.crc32_batch_host_packed(host, offs, lens)
+    if os.environ.get("CIO_BENCH_PRE_ALLOC_GB") and alloc_after:
+        big_alloc()
     barrier(dist)
     t0 = time.perf_counter()
     steps = max(1, min(args.steps, 30))
@@ -1041,7 +1066,11 @@ def other_chunk_sizes(args, rank, world, device, dist):
     import copy
     import torch
     out = {}
-    for cfg, steps, warm in (("cfg4k", 200, 50), ("cfg4", 20, 5)):
+    sizes = (("cfg4k", 200, 50), ("cfg4", 20, 5))
+    if os.environ.get("CIO_BENCH_SIZES") is not None:
+        # diagnostic: a subset of the sizes (e.g. "" for none, "cfg4k")
+        sizes = tuple(x for x in sizes if x[0] in os.environ["CIO_BENCH_SIZES"].split(","))
+    for cfg, steps, warm in sizes:
         torch.cuda.empty_cache()
         a = copy.copy(args)
         a.config, a.steps, a.warmup, a.no_cpu = cfg, steps, warm, True
@@ -1169,7 +1198,7 @@ def spawn_ranks(args):
             signal.signal(sig, h)
 
 
-def other_configs(args, rank, world, device, dist):
+def other_configs(args, rank, world, device, dist, only=None):
     """The north star's other single-GPU workloads, short runs in the same
     process so the default line carries every config: cfg3 (65,536 mixed
     4 KB-4 MB chunks, ~39.7 GB, persistent load-balanced kernel), cfg5 (SHA-1
@@ -1185,6 +1214,8 @@ def other_configs(args, rank, world, device, dist):
         # verify-on-load of 1000 chunk files, and the config-1 loop through
         # the C chunk layer with deferred CRC + batched GPU sync.
         legs += [("verify", 3, 1), ("perf", 2, 1)]
+    if only is not None:
+        legs = [leg for leg in legs if leg[0] in only]
     if os.environ.get("CIO_BENCH_LEGS"):
         # diagnostic: a subset / order of the legs (e.g. "e2e,cfg3")
         by = {cfg: (cfg, s, w) for cfg, s, w in legs}
@@ -1238,8 +1269,18 @@ def main():
     else:
         res = run_crc(args, rank, world, device, dist)
         if args.config == "cfg2" and not args.no_extra:
+            # The host-memory legs (e2e, verify, perf) run before the legs
+            # that allocate and free tens of GB of HBM (cfg4: 34 GB, cfg3:
+            # 40 GB): the driver clears freed VRAM in the background on the
+            # SDMA engines the H2D copies use, which slows host batches by
+            # ~11% for ~1 s after such a free (profiles/r04/e2e_vram_free_*).
+            host_legs = other_configs(args, rank, world, device, dist, only=("e2e", "verify", "perf"))
             res["other_chunk_sizes"] = other_chunk_sizes(args, rank, world, device, dist)
-            res["other_configs"] = other_configs(args, rank, world, device, dist)
+            dev_legs = other_configs(args, rank, world, device, dist, only=("cfg3", "sha1"))
+            wall = host_legs.pop("wall_s") + dev_legs.pop("wall_s")
+            res["other_configs"] = {**dev_legs, **host_legs, "wall_s": round(wall, 2),
+                                    "order": "run order: e2e, verify, perf (host-memory legs, before any "
+                                             "multi-GB HBM free), then other_chunk_sizes, cfg3, sha1"}
             res["diagnostic_batches"] = diagnostic_batches(device)
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -16,7 +16,10 @@ import sys
 def main():
     copies = [r for r in csv.DictReader(open(sys.argv[1])) if "HOST_TO_DEVICE" in r["Direction"]]
     gap = float(sys.argv[3]) if len(sys.argv) > 3 else 500.0
-    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id", "")) for r in copies)
+    szk = next((k for k in (copies[0].keys() if copies else []) if "size" in k.lower() or "bytes" in k.lower()), None)
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                 r.get("Stream_Id", "") + (f" {int(r[szk]) / 1e6:8.1f} MB {int(r[szk]) / max(1, int(r['End_Timestamp']) - int(r['Start_Timestamp'])):6.1f} GB/s" if szk else ""))
+                for r in copies)
     calls, cur, end = [], [], None
     for s, e, st in ev:
         if cur and (s - end) / 1e3 > gap:
@@ -46,7 +49,7 @@ def main():
               f"largest idle gap {max(idle) if idle else 0:6.1f} us")
     last = calls[-1]
     t0 = last[0][0]
-    print("last call's copies: start_us dur_us stream")
+    print("last call's copies: start_us dur_us stream [MB GB/s]")
     for s, e, st in last:
         print(f"  {(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {st}")
 
