@@ -501,26 +501,13 @@ void slot_free(PipeSlot &s)
     s = PipeSlot();
 }
 
-// A/B knob (read once): 0 = each slot's device buffer is kStage + 64 bytes,
-// 1 = rounded up to a 2 MiB multiple.
-static int dbuf_mode()
-{
-    static const int v = [] {
-        const char *r = getenv("CIO_GPU_DBUF_MODE");
-        return r ? atoi(r) : 0;
-    }();
-    return v;
-}
-
 hipError_t pipe_init(HostPipe &hp, int dev)
 {
     hipError_t e = hipSuccess;
-    const size_t dbytes = dbuf_mode() == 1 ? ((kStage + 64 + (2u << 20) - 1) & ~(size_t) ((2u << 20) - 1))
-                                           : kStage + 64;
     for (int b = 0; b < kSlots && e == hipSuccess; b++) {
         PipeSlot &s = hp.slot[b];
         if ((e = hipHostMalloc(&s.pinned, kStage, hipHostMallocDefault)) != hipSuccess) break;
-        if ((e = hipMalloc(&s.dbuf, dbytes)) != hipSuccess) break;
+        if ((e = hipMalloc(&s.dbuf, kStage + 64)) != hipSuccess) break;
         if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess) break;
         e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     }
