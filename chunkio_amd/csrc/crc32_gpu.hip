@@ -753,7 +753,13 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         // compiler's vmcnt waits stay exact, and the table is L2-resident.
         if (AHEAD) {
             const bool real = nload > 0;
-            const uint8_t *src = real ? lbase + ld.a : reinterpret_cast<const uint8_t *>(g_slice);
+            // Uniform batches re-read chunk 0's first step instead (base and
+            // ua0 are preloaded SGPRs): the table pointer is a kernel argument
+            // the hardware does not preload, and its scalar load held every
+            // wave's first HBM request.
+            const uint8_t *src = real ? lbase + ld.a
+                               : (UNIFORM && !CIO_AHEAD_DUMMY_SLICE) ? base + ua0
+                                                                      : reinterpret_cast<const uint8_t *>(g_slice);
             if (L64) {
                 load_step64(r, src, real ? lj : 0, lane);
             } else {
@@ -805,8 +811,15 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // latency overlaps it (requesting two was slower: profiles/r01/ab_v4_steps.txt).
     // Unconditional (also for inactive waves): a branch here would merge a
     // no-load path into the vmcnt state and make the table build wait for the ring.
-    StepRegs cur;
+    StepRegs cur, nxt;
     issue(cur);
+#if CIO_AHEAD_PRE2
+    if (AHEAD) {
+        // The second step goes out with the first, so the memory system has
+        // work while the tables are built (else step 1 waits for them).
+        issue(nxt);
+    }
+#endif
     // The data requests leave first; the bookkeeping loads below need
     // kernel-argument pointers (scalar loads) and must not hold them back.
     __builtin_amdgcn_sched_barrier(0);
@@ -1013,7 +1026,6 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             // goes out before this slot's CRC: the compiler's wait for this
             // slot is then vmcnt(4) (the refill's four loads may stay in
             // flight), and the wave keeps 4 KiB in flight while it computes.
-            StepRegs nxt;
             // The slot's data must have landed before the refill goes out
             // (else both slots are in flight, 8 KiB per wave, which measured
             // slower): an empty asm reading the 16 data registers makes the
@@ -1048,7 +1060,24 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                 }
             };
             using Refill = std::true_type;
-#if CIO_AHEAD_PEEL
+#if CIO_AHEAD_PRE2
+            // Step 1 is already in flight in nxt: step 0 refills nothing, the
+            // slots then alternate from step 1, and the last step refills
+            // nothing (iters issues in all).
+            using NoRefill = std::false_type;
+            half(0, cur, nxt, NoRefill());
+            uint64_t it = 1;
+            for (; it + 2 < iters; it += 2) {
+                half(it, nxt, cur, Refill());
+                half(it + 1, cur, nxt, Refill());
+            }
+            if (iters - it == 2) {
+                half(it, nxt, cur, Refill());
+                half(it + 1, cur, nxt, NoRefill());
+            } else if (iters - it == 1) {
+                half(it, nxt, cur, NoRefill());
+            }
+#elif CIO_AHEAD_PEEL
             // The wave's last step is peeled off the loop: it issues no
             // refill, so the wave does not end waiting for four loads nobody
             // reads (the refill past the range re-reads the slice table; its
