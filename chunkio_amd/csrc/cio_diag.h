@@ -50,24 +50,6 @@
 #define CIO_AHEAD_PEEL 1
 #endif
 
-/* A/B: loads past a wave's range in the issue-ahead kernel read the slice
- * table (1, round 3) or, in uniform batches, chunk 0's first step (0). */
-#ifndef CIO_AHEAD_DUMMY_SLICE
-#define CIO_AHEAD_DUMMY_SLICE 0
-#endif
-
-/* A/B: the issue-ahead stream kernel requests its first TWO steps before the
- * table build (1), or only the first (0, shipped). */
-#ifndef CIO_AHEAD_PRE2
-#define CIO_AHEAD_PRE2 0
-#endif
-
-/* A/B: the stream kernel builds its LDS tables before (1) or after (0,
- * shipped) requesting its first step's data. */
-#ifndef CIO_TABLES_FIRST
-#define CIO_TABLES_FIRST 0
-#endif
-
 /* Small-chunk kernel.  A/B: chunks in flight per wave (1 shipped, 2).
  * Diagnostic bit mask: 1 = no lane multiply, 2 = no LDS CRC (wrong CRCs). */
 #ifndef CIO_SMALL_SLOTS

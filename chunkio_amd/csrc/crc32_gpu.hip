@@ -758,8 +758,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
             // the hardware does not preload, and its scalar load held every
             // wave's first HBM request.
             const uint8_t *src = real ? lbase + ld.a
-                               : (UNIFORM && !CIO_AHEAD_DUMMY_SLICE) ? base + ua0
-                                                                      : reinterpret_cast<const uint8_t *>(g_slice);
+                               : UNIFORM ? base + ua0 : reinterpret_cast<const uint8_t *>(g_slice);
             if (L64) {
                 load_step64(r, src, real ? lj : 0, lane);
             } else {
@@ -803,23 +802,12 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         }
         write_tables<STAMPS>(lds, tid, tab_v, tab_sv, t_wt);
     };
-#if CIO_TABLES_FIRST
-    build_tables();
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     // The first step is requested before the table build so that its HBM
     // latency overlaps it (requesting two was slower: profiles/r01/ab_v4_steps.txt).
     // Unconditional (also for inactive waves): a branch here would merge a
     // no-load path into the vmcnt state and make the table build wait for the ring.
     StepRegs cur, nxt;
     issue(cur);
-#if CIO_AHEAD_PRE2
-    if (AHEAD) {
-        // The second step goes out with the first, so the memory system has
-        // work while the tables are built (else step 1 waits for them).
-        issue(nxt);
-    }
-#endif
     // The data requests leave first; the bookkeeping loads below need
     // kernel-argument pointers (scalar loads) and must not hold them back.
     __builtin_amdgcn_sched_barrier(0);
@@ -866,9 +854,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
         t_issued = __builtin_amdgcn_s_memrealtime();
     }
 
-#if !CIO_TABLES_FIRST
     build_tables();
-#endif
     __syncthreads();
     if (STAMPS) {
         t_tables = __builtin_amdgcn_s_memrealtime();
@@ -1060,24 +1046,7 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                 }
             };
             using Refill = std::true_type;
-#if CIO_AHEAD_PRE2
-            // Step 1 is already in flight in nxt: step 0 refills nothing, the
-            // slots then alternate from step 1, and the last step refills
-            // nothing (iters issues in all).
-            using NoRefill = std::false_type;
-            half(0, cur, nxt, NoRefill());
-            uint64_t it = 1;
-            for (; it + 2 < iters; it += 2) {
-                half(it, nxt, cur, Refill());
-                half(it + 1, cur, nxt, Refill());
-            }
-            if (iters - it == 2) {
-                half(it, nxt, cur, Refill());
-                half(it + 1, cur, nxt, NoRefill());
-            } else if (iters - it == 1) {
-                half(it, nxt, cur, NoRefill());
-            }
-#elif CIO_AHEAD_PEEL
+#if CIO_AHEAD_PEEL
             // The wave's last step is peeled off the loop: it issues no
             // refill, so the wave does not end waiting for four loads nobody
             // reads (the refill past the range re-reads the slice table; its
