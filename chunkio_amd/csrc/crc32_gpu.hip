@@ -1869,11 +1869,13 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
         p->l64 = p->l64_small = atoi(r) != 0;
     }
     p->grid = (uint32_t) st->cus;
-    // Test knob: fewer workgroups than CUs (e.g. a wave count that is not a
-    // power of two, which takes the kernels' f64 split instead of the shift).
+    // Test / A/B knob: another workgroup count (fewer than CUs: e.g. a wave
+    // count that is not a power of two, which takes the kernels' f64 split
+    // instead of the shift; more: workgroups that queue for a CU, up to 16
+    // per CU).
     if (const char *r = getenv("CIO_GPU_GRID")) {
         const int v = atoi(r);
-        if (v >= 1 && v < (int) p->grid) {
+        if (v >= 1 && v <= 16 * (int) p->grid) {
             p->grid = (uint32_t) v;
         }
     }
@@ -1906,8 +1908,9 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
         bytes += lens[i];
     }
     // The kernels' start-up divisions (div_u52) need w * S < 2^52 for w <= W
-    // <= 2^12: 2^40 wave-steps is 4 PiB, far past any device's memory.
-    if (S >= (1ull << 40) || W > 4096) {
+    // (W <= 2^12 on a full device: 2^40 wave-steps is 4 PiB, far past any
+    // device's memory).
+    if (S >= (1ull << 40) || W > 65536 || (S * (uint64_t) W) >> 52) {
         return "cio_crc32_plan_create: batch too large";
     }
     ph.S = S;
@@ -2062,10 +2065,24 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         delete p;
         return fail(err);
     }
+    plan_uniform(p, offs, lens, n, ph);
+    // Long mixed-size batches (>= 1 MiB per wave, e.g. cfg3's ~2400 steps per
+    // wave) split over 4 workgroups per CU: the extra workgroups queue for a
+    // CU and start wherever one finishes, so the hardware evens out the
+    // per-CU finish times (cfg3 -0.7 %; uniform batches lose, cfg2 +5 %, 4 MiB
+    // chunks +0.8 %: profiles/r04/ab_grid_oversubscribed_r04q.txt).
+    if (p->unsteps == 0 && !getenv("CIO_GPU_GRID") && ph.S >= 256ull * p->W && 4ull * p->W <= 65536 &&
+        ph.S != (uint64_t) n - ph.tiny.size()) {    // (not a small-chunk batch)
+        PlanHost ph4;
+        if (plan_build(ph4, offs, lens, n, 4 * p->W) == nullptr) {
+            p->grid *= 4;
+            p->W *= 4;
+            ph = std::move(ph4);
+        }
+    }
     p->S = ph.S;
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
-    plan_uniform(p, offs, lens, n, ph);
     // Uniform batch of whole 4 KiB steps, 16-byte aligned, with short wave
     // ranges (<= 64 steps, e.g. cfg2's 25): the issue-ahead stream kernel.
     // Interleaved A/Bs (profiles/r03/ab_issue_ahead_*.txt): cfg2 -0.6 to

@@ -270,8 +270,8 @@ def test_reduced_grid_split_paths(cuda, monkeypatch, grid):
 def test_issue_ahead_uniform_aligned_batches(cuda, monkeypatch, grid, l64):
     """The issue-ahead stream kernel (uniform batches of whole 4 KiB steps at
     16-byte-aligned offsets: two ring slots, the refill issued once the
-    current slot has landed, dummy refills past the range from the slice
-    table) against the oracle and against the one-slot kernel
+    current slot has landed, dummy refills past the range from chunk 0's
+    first step) against the oracle and against the one-slot kernel
     (CIO_GPU_AHEAD=0): odd and even step counts per wave, one step per
     wave, fewer steps than waves, chunks spanning many waves and
     workgroups, seeds; on the full grid and a 48-wave grid (f64 split)."""
