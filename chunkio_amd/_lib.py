@@ -20,14 +20,14 @@ EXPORTS = (
     "cio_gpu_init", "cio_gpu_last_error", "cio_gpu_version",
     "cio_crc32_shift", "cio_crc32_combine",
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
-    "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_batch_dev", "cio_crc32_batch_host",
+    "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_plan_workgroups", "cio_crc32_batch_dev", "cio_crc32_batch_host",
     "cio_crc32_batch_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device", "cio_gpu_numa_node",
     "cio_crc32_host_register", "cio_crc32_host_unregister", "cio_gpu_pipe_last_timing",
     "cio_crc32_cpu_max", "cio_crc32_set_cpu_max", "cio_crc32_host_threads", "cio_crc32_set_host_threads",
     "cio_crc32_route_reset",
     "cio_crc32_batch_cpu", "cio_crc32_batch_fd_cpu",
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_sha1_batch_dev_async",
-    "cio_sha1_state_init", "cio_sha1_update_batch_dev", "cio_sha1_final_batch_dev", "cio_gpu_read_stream",
+    "cio_sha1_state_init", "cio_sha1_update_batch_dev", "cio_sha1_final_batch_dev", "cio_gpu_read_stream", "cio_gpu_read_stream_grid",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
     # include/chunkio_amd/cio_verify.h
@@ -70,6 +70,7 @@ def _bind(lib):
         "cio_crc32_plan_exec_events": (ctypes.c_int, [V, V, V, V, V, V, V]),
         "cio_crc32_plan_bytes": (ctypes.c_uint64, [V]),
         "cio_crc32_plan_kernel": (ctypes.c_char_p, [V]),
+        "cio_crc32_plan_workgroups": (ctypes.c_uint32, [V]),
         "cio_crc32_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, V, ctypes.c_size_t, V]),
         "cio_crc32_batch_host": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p,
                                                 ctypes.c_size_t]),
@@ -99,6 +100,7 @@ def _bind(lib):
         "cio_sha1_update_batch_dev": (ctypes.c_int, [V, V, V, V, ctypes.c_size_t, V]),
         "cio_sha1_final_batch_dev": (ctypes.c_int, [V, V, ctypes.c_size_t, V]),
         "cio_gpu_read_stream": (ctypes.c_int, [V, ctypes.c_uint64, V]),
+        "cio_gpu_read_stream_grid": (ctypes.c_int, [V, ctypes.c_uint64, ctypes.c_uint32, V]),
         "cio_gpu_event_create": (V, []),
         "cio_gpu_event_destroy": (None, [V]),
         "cio_gpu_event_record": (ctypes.c_int, [V, V]),

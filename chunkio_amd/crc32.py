@@ -97,6 +97,11 @@ class Crc32Plan:
     def bytes(self):
         return int(_lib.lib().cio_crc32_plan_bytes(self._handle))
 
+    @property
+    def workgroups(self):
+        """Workgroups one launch runs (one per CU, or four for long mixed batches)."""
+        return int(_lib.lib().cio_crc32_plan_workgroups(self._handle))
+
     def kernel_name(self):
         """The kernel this plan launches (crc32_stream_kernel / crc32_small_kernel)."""
         return _lib.lib().cio_crc32_plan_kernel(self._handle).decode()

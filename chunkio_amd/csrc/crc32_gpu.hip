@@ -2169,6 +2169,11 @@ uint64_t cio_crc32_plan_bytes(const cio_crc32_plan *p)
     return p ? p->bytes : 0;
 }
 
+uint32_t cio_crc32_plan_workgroups(const cio_crc32_plan *p)
+{
+    return p ? p->grid : 0;
+}
+
 const char *cio_crc32_plan_kernel(const cio_crc32_plan *p)
 {
     return (p && p->small) ? "crc32_small_kernel" : "crc32_stream_kernel";
@@ -2350,11 +2355,20 @@ int cioa_debug_rs_stamps(unsigned long long *host, size_t cap)
     return (int) g_rs_waves;
 }
 
-static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, hipEvent_t ev0, hipEvent_t ev1);
+static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, hipEvent_t ev0, hipEvent_t ev1,
+                            uint32_t workgroups = 0);
 
 int cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream)
 {
     return read_stream_impl(dev_base, bytes, stream, nullptr, nullptr);
+}
+
+int cio_gpu_read_stream_grid(const void *dev_base, uint64_t bytes, uint32_t workgroups, void *stream)
+{
+    if (workgroups > 65536 / (kThreads / kWave)) {
+        return fail("cio_gpu_read_stream_grid: more than 4096 workgroups");
+    }
+    return read_stream_impl(dev_base, bytes, stream, nullptr, nullptr, workgroups);
 }
 
 /* Diagnostic (not in the public header): the read-only stream with events
@@ -2365,12 +2379,14 @@ int cioa_debug_read_stream_events(const void *dev_base, uint64_t bytes, void *st
                             reinterpret_cast<hipEvent_t>(ev1));
 }
 
-static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, hipEvent_t ev0, hipEvent_t ev1)
+static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, hipEvent_t ev0, hipEvent_t ev1,
+                            uint32_t workgroups)
 {
     DeviceState *st;
     if (device_state(&st) != CIO_OK) {
         return CIO_ERROR;
     }
+    const uint32_t grid = workgroups ? workgroups : (uint32_t) st->cus;
     static thread_local uint32_t *sink = nullptr;
     if (!sink) {
         HIP_TRY(hipMalloc(&sink, 65536 * sizeof(uint32_t)), "read_stream: hipMalloc");
@@ -2431,7 +2447,7 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
     }
-    hipLaunchKernelGGL(read_stream_kernel, dim3(st->cus), dim3(kThreads), 0,
+    hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream),
                        reinterpret_cast<const uint8_t *>(dev_base), S, sink, B, stamps, work);
     HIP_TRY(hipGetLastError(), "read_stream_kernel launch");

@@ -125,6 +125,10 @@ uint64_t cio_crc32_plan_bytes(const cio_crc32_plan *plan);
  * batches) or "crc32_small_kernel" (every chunk within one 4 KiB wave-step). */
 const char *cio_crc32_plan_kernel(const cio_crc32_plan *plan);
 
+/* Workgroups one launch of the plan runs (one per CU; four per CU for long
+ * mixed-size batches, whose extra workgroups queue for a free CU). */
+uint32_t cio_crc32_plan_workgroups(const cio_crc32_plan *plan);
+
 /* One-shot: plan + exec + wait + destroy. */
 int  cio_crc32_batch_dev(const void *dev_base, const uint64_t *offs,
                          const uint64_t *lens, const uint32_t *dev_seeds,
@@ -285,6 +289,10 @@ int  cio_sha1_final_batch_dev(const cio_sha1_state *dev_states, uint8_t *dev_dig
  * CRC kernel's grid and load pattern (no CRC): the practical HBM-read ceiling
  * the CRC kernel is measured against.  Asynchronous on `stream`. */
 int  cio_gpu_read_stream(const void *dev_base, uint64_t bytes, void *stream);
+
+/* The same on `workgroups` 1024-thread workgroups (0 = one per CU, <= 4096):
+ * the ceiling for a plan that runs cio_crc32_plan_workgroups(plan) of them. */
+int  cio_gpu_read_stream_grid(const void *dev_base, uint64_t bytes, uint32_t workgroups, void *stream);
 
 /* ---- timing helpers (HIP events on a given stream) --------------------- */
 

@@ -373,6 +373,25 @@ def test_cfg3_mixed_sizes_full(cuda, golden):
     split_combine_check(cuda, dev, offs, lens, got)
 
 
+def test_plan_workgroups(cuda, monkeypatch):
+    """Long mixed-size batches (>= 1 MiB per wave) plan 4 workgroups per CU,
+    uniform and small-chunk batches one; CIO_GPU_GRID overrides.  (Parity of
+    the 4x grid: test_cfg3_mixed_sizes_full, whose geometry takes it.)"""
+    cus = __import__("torch").cuda.get_device_properties(cuda).multi_processor_count
+    l3 = wl.cfg3_lens()
+    with cio.Crc32Plan(wl.packed_offsets(l3), l3) as p3:
+        assert p3.workgroups == 4 * cus
+    l2 = wl.cfg2_lens()
+    with cio.Crc32Plan(wl.packed_offsets(l2, align=16), l2) as p2:
+        assert p2.workgroups == cus
+    l4 = np.full(8192, 4 << 20, np.uint64)      # uniform, 2 MiB per wave: one per CU
+    with cio.Crc32Plan(wl.packed_offsets(l4), l4) as p4:
+        assert p4.workgroups == cus
+    monkeypatch.setenv("CIO_GPU_GRID", "17")
+    with cio.Crc32Plan(wl.packed_offsets(l3), l3) as p3:
+        assert p3.workgroups == 17
+
+
 def test_cfg4_shard_golden(cuda, golden):
     import torch
     g = golden["cfg4"]
