@@ -300,6 +300,44 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
     return res
 
 
+def cpu_sample_baseline(dev_buf, offs, lens, gpu_out, max_bytes=1 << 30):
+    """SURVEY §8(d) CPU item 2 for the cfg3 / cfg4 batches: the reference's
+    crc_update (oracle/_ref) on 1 thread and on the box's per-GPU CPU share,
+    over a bounded sample of the same batch (its first chunks, <= 1 GiB,
+    copied from HBM), each result checked against the GPU's."""
+    import ctypes
+    from oracle import pyoracle as po
+    lib = po.ref()
+    kind, prefix = "reference", "ref_"
+    if lib is None:
+        lib, kind, prefix = po.oracle(), "port", "oracle_"
+    k = int(max(1, np.searchsorted(np.cumsum(lens.astype(np.uint64)), max_bytes, side="right")))
+    k = min(k, len(lens))
+    lo, hi = int(offs[0]), int(offs[k - 1] + lens[k - 1])
+    host = dev_buf[lo:hi].cpu().numpy()
+    o = np.ascontiguousarray(offs[:k] - offs[0], dtype=np.uint64)
+    ln = np.ascontiguousarray(lens[:k], dtype=np.uint64)
+    u64p, u32p = ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)
+    out = np.zeros(k, dtype=np.uint32)
+    secs = getattr(lib, prefix + "crc_batch_time")(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p),
+                                                     k, 1, out.ctypes.data_as(u32p))
+    res = {"value": round(float(ln.sum()) / secs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
+           "sample": f"the batch's first {k} chunks ({int(ln.sum())} B, copied from HBM), one pass, "
+                     f"crc_update(init, chunk) per chunk",
+           "bit_exact_vs_gpu": bool(np.array_equal(out, gpu_out[:k]))}
+    f_mt = getattr(lib, prefix + "crc_batch_time_mt", None)
+    if f_mt is not None:
+        f_mt.restype = ctypes.c_double
+        f_mt.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, u32p]
+        nt = host_cpu_threads()
+        out_mt = np.zeros(k, dtype=np.uint32)
+        secs_mt = f_mt(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), k, 2, nt,
+                       out_mt.ctypes.data_as(u32p))
+        res["multi_thread"] = {"value": round(float(ln.sum()) * 2 / secs_mt / 1e9, 3), "unit": "GB/s", "threads": nt,
+                               "bit_exact_vs_gpu": bool(np.array_equal(out_mt, gpu_out[:k]))}
+    return res
+
+
 def run_crc(args, rank, world, device, dist):
     import torch
     import chunkio_amd as cio
@@ -513,6 +551,11 @@ def run_crc(args, rank, world, device, dist):
     if rank == 0 and world == 1 and not args.no_cpu and args.config == "cfg2":
         host = bufs[0].cpu().numpy()
         res["cpu_baseline"] = cpu_baseline(host, offs, lens, gpu0)
+    if rank == 0 and world == 1 and args.config in ("cfg3", "cfg4") and not getattr(args, "no_cpu_sample", args.no_cpu):
+        try:
+            res["cpu_baseline"] = cpu_sample_baseline(bufs[0], offs, lens, gpu0)
+        except Exception as e:  # informational
+            res["cpu_baseline"] = {"error": str(e)}
     plan.close()
     return res
 
@@ -1076,12 +1119,15 @@ def other_chunk_sizes(args, rank, world, device, dist):
         torch.cuda.empty_cache()
         a = copy.copy(args)
         a.config, a.steps, a.warmup, a.no_cpu = cfg, steps, warm, True
+        a.no_cpu_sample = args.no_cpu
         r = run_crc(a, rank, world, device, dist)
         out[cfg] = {"value": r["value"], "unit": r["unit"], "scaling": r["scaling"], "steps": steps,
                     "warmup": warm, "ms_per_step": r["ms_per_step"], "workload": r["config"]["workload"],
                     "roofline": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "kernel",
                                                                 "kernel_ms_mean", "traffic")},
                     "check": r.get("check", {})}
+        if "cpu_baseline" in r:
+            out[cfg]["cpu_baseline"] = r["cpu_baseline"]
         if "per_gpu" in r:
             out[cfg]["per_gpu"] = r["per_gpu"]
     torch.cuda.empty_cache()
@@ -1227,6 +1273,7 @@ def other_configs(args, rank, world, device, dist, only=None):
         a = copy.copy(args)
         a.config, a.steps, a.warmup = cfg, steps, warm
         a.no_cpu = cfg != "verify" or args.no_cpu
+        a.no_cpu_sample = args.no_cpu
         t1 = time.perf_counter()
         if cfg == "sha1":
             r = run_sha1(a, rank, world, device, dist)
