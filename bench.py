@@ -625,39 +625,58 @@ def run_sha1(args, rank, world, device, dist):
             "check": check}
 
 
+class E2eDiag:
+    """Diagnostic preambles of the e2e leg (profiles/r04/e2e_vram_free/README.md),
+    all off by default: CIO_BENCH_PRE_STREAMS=k creates k HIP streams (each
+    having run work) before the pipeline's own; CIO_BENCH_PRE_ALLOC_GB=g
+    allocates, writes and frees g GB of HBM before the pipeline is created,
+    or after its warmup calls with CIO_BENCH_ALLOC_AFTER_WARM=1, then sleeps
+    CIO_BENCH_ALLOC_SETTLE_S seconds."""
+
+    def __init__(self, device):
+        self.device = device
+        self.streams = []
+        self.gb = float(os.environ.get("CIO_BENCH_PRE_ALLOC_GB", "0"))
+        self.after = os.environ.get("CIO_BENCH_ALLOC_AFTER_WARM") == "1"
+
+    def _alloc(self):
+        import torch
+        big = torch.empty(int(self.gb * 1e9), dtype=torch.uint8, device=self.device)
+        big.fill_(1)
+        torch.cuda.synchronize(self.device)
+        del big
+        torch.cuda.empty_cache()
+        time.sleep(float(os.environ.get("CIO_BENCH_ALLOC_SETTLE_S", "0")))
+
+    def before_pipeline(self):
+        k = int(os.environ.get("CIO_BENCH_PRE_STREAMS", "0"))
+        if k:
+            import torch
+            for _ in range(k):
+                st = torch.cuda.Stream(self.device)
+                with torch.cuda.stream(st):
+                    torch.ones(16, device=self.device).sum()
+                self.streams.append(st)
+            torch.cuda.synchronize(self.device)
+        if self.gb and not self.after:
+            self._alloc()
+
+    def after_warmup(self):
+        if self.gb and self.after:
+            self._alloc()
+
+
 def run_e2e(args, rank, world, device, dist):
     import chunkio_amd as cio
     from chunkio_amd import workloads as wl
     lens, ids, seed, desc, scaling = geometry("e2e", rank, world)
     bound = bind_to_gpu_node(device.index or 0)
-    pre = []
-    if os.environ.get("CIO_BENCH_PRE_STREAMS"):
-        # diagnostic: streams that exist (and have run work) before the
-        # pipeline's own streams are created
-        import torch
-        for _ in range(int(os.environ["CIO_BENCH_PRE_STREAMS"])):
-            st_ = torch.cuda.Stream(device)
-            with torch.cuda.stream(st_):
-                torch.ones(16, device=device).sum()
-            pre.append(st_)
-        torch.cuda.synchronize(device)
-    def big_alloc():
-        # diagnostic: a large device allocation made, written and freed
-        import torch
-        big = torch.empty(int(float(os.environ["CIO_BENCH_PRE_ALLOC_GB"]) * 1e9), dtype=torch.uint8, device=device)
-        big.fill_(1)
-        torch.cuda.synchronize(device)
-        del big
-        torch.cuda.empty_cache()
-        time.sleep(float(os.environ.get("CIO_BENCH_ALLOC_SETTLE_S", "0")))
-    alloc_after = os.environ.get("CIO_BENCH_ALLOC_AFTER_WARM") == "1"
-    if os.environ.get("CIO_BENCH_PRE_ALLOC_GB") and not alloc_after:
-        big_alloc()
+    diag = E2eDiag(device)
+    diag.before_pipeline()
     host, offs = wl.host_batch(seed, lens, align=16)
     for _ in range(max(1, args.warmup)):
         out = cio.crc32_batch_host_packed(host, offs, lens)
-    if os.environ.get("CIO_BENCH_PRE_ALLOC_GB") and alloc_after:
-        big_alloc()
+    diag.after_warmup()
     barrier(dist)
     t0 = time.perf_counter()
     steps = max(1, min(args.steps, 30))

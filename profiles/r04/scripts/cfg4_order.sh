@@ -1,6 +1,6 @@
 #!/bin/bash
 # cfg4 (8192 x 4 MiB at N = 1) standalone, in the default line, and in the
-# default line without its host-memory legs.  Usage: bash tools/cfg4_order.sh TAG
+# default line without its host-memory legs.  Usage: bash profiles/r04/scripts/cfg4_order.sh TAG
 set -u
 D=gpurun_out/$1; mkdir -p $D
 timeout -k 10 200 python bench.py --config cfg4 --steps 20 --warmup 5 --no-cpu > $D/cfg4_alone.json 2> $D/cfg4_alone.err || exit $?

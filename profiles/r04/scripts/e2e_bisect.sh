@@ -1,7 +1,7 @@
 #!/bin/bash
 # Default line reduced to its cfg2 leg + the e2e leg, with parts of the cfg2
 # leg switched off.  Each argument: "NAME|ENV=..,ENV=..|bench flags".
-# Usage: bash tools/e2e_bisect.sh TAG "full||" "nocpu||--no-cpu" ...
+# Usage: bash profiles/r04/scripts/e2e_bisect.sh TAG "full||" "nocpu||--no-cpu" ...
 set -u
 TAG=$1; shift; D=gpurun_out/$TAG; mkdir -p $D
 for spec in "$@"; do

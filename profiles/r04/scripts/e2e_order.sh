@@ -1,7 +1,7 @@
 #!/bin/bash
 # Which earlier leg of the default line slows its e2e leg: the default line
 # with only some legs, in a given order (CIO_BENCH_LEGS), e2e values printed.
-# Usage: bash tools/e2e_order.sh TAG "e2e" "cfg3,e2e" ...
+# Usage: bash profiles/r04/scripts/e2e_order.sh TAG "e2e" "cfg3,e2e" ...
 set -u
 TAG=$1; shift; D=gpurun_out/$TAG; mkdir -p $D
 i=0

@@ -1,7 +1,7 @@
 #!/bin/bash
 # E2E host-pipeline probe: the driver's default line and a standalone e2e
 # line, each with per-call pipeline legs on stderr (CIO_GPU_PIPE_TIMING=1).
-# Usage: bash tools/e2e_probe.sh TAG
+# Usage: bash profiles/r04/scripts/e2e_probe.sh TAG
 set -u
 TAG=$1; D=gpurun_out/$TAG; mkdir -p $D
 CIO_GPU_PIPE_TIMING=1 timeout -k 10 400 python bench.py > $D/default.json 2> $D/default.err || exit $?

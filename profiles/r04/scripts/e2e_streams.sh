@@ -1,6 +1,6 @@
 #!/bin/bash
 # Standalone e2e lines with k streams created before the pipeline's own
-# (CIO_BENCH_PRE_STREAMS=k).  Usage: bash tools/e2e_streams.sh TAG k1 k2 ...
+# (CIO_BENCH_PRE_STREAMS=k).  Usage: bash profiles/r04/scripts/e2e_streams.sh TAG k1 k2 ...
 set -u
 TAG=$1; shift; D=gpurun_out/$TAG; mkdir -p $D
 for k in "$@"; do

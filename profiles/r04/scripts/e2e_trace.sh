@@ -1,7 +1,7 @@
 #!/bin/bash
 # Copy/kernel timelines of the standalone e2e line with and without a prior
 # 34.4 GB device allocation (CIO_BENCH_PRE_ALLOC_GB): rocprofv3 kernel +
-# memory-copy trace, no counters.  Usage: bash tools/e2e_trace.sh TAG
+# memory-copy trace, no counters.  Usage: bash profiles/r04/scripts/e2e_trace.sh TAG
 set -u
 OUT=gpurun_out/$1; mkdir -p $OUT
 export TMPDIR=/tmp
