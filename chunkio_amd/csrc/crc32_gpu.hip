@@ -2066,12 +2066,13 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         return fail(err);
     }
     plan_uniform(p, offs, lens, n, ph);
-    // Long mixed-size batches (>= 1 MiB per wave, e.g. cfg3's ~2400 steps per
-    // wave) split over 4 workgroups per CU: the extra workgroups queue for a
-    // CU and start wherever one finishes, so the hardware evens out the
-    // per-CU finish times (cfg3 -0.7 %; uniform batches lose, cfg2 +5 %, 4 MiB
-    // chunks +0.8 %: profiles/r04/ab_grid_oversubscribed_r04q.txt).
-    if (p->unsteps == 0 && !getenv("CIO_GPU_GRID") && ph.S >= 256ull * p->W && 4ull * p->W <= 65536 &&
+    // Long batches (>= 4 MiB per wave: cfg3's ~2400 steps per wave, cfg4's
+    // 2048 at one GPU) split over 4 workgroups per CU: the extra workgroups
+    // queue for a CU and start wherever one finishes, so the hardware evens
+    // out the per-CU finish times (cfg3 -0.7 %, cfg4 -1.7 %; shorter ranges
+    // lose: 1 MiB per wave +0.8 to +5.5 %, cfg2 +5 %:
+    // profiles/r04/ab_grid_oversubscribed_r04q.txt, ab_grid_cfg4_r04x.txt).
+    if (!getenv("CIO_GPU_GRID") && ph.S >= 1024ull * p->W && 4ull * p->W <= 65536 &&
         ph.S != (uint64_t) n - ph.tiny.size()) {    // (not a small-chunk batch)
         PlanHost ph4;
         if (plan_build(ph4, offs, lens, n, 4 * p->W) == nullptr) {

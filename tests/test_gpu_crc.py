@@ -374,9 +374,10 @@ def test_cfg3_mixed_sizes_full(cuda, golden):
 
 
 def test_plan_workgroups(cuda, monkeypatch):
-    """Long mixed-size batches (>= 1 MiB per wave) plan 4 workgroups per CU,
-    uniform and small-chunk batches one; CIO_GPU_GRID overrides.  (Parity of
-    the 4x grid: test_cfg3_mixed_sizes_full, whose geometry takes it.)"""
+    """Long batches (>= 4 MiB per wave: cfg3, cfg4 at one GPU) plan 4
+    workgroups per CU, shorter ones (cfg2, 1024 x 4 MiB) one; CIO_GPU_GRID
+    overrides.  (Parity of the 4x grid: test_cfg3_mixed_sizes_full and
+    test_cfg4_full_job_sharded_g1_2_4_8's one-GPU shard take it.)"""
     cus = __import__("torch").cuda.get_device_properties(cuda).multi_processor_count
     l3 = wl.cfg3_lens()
     with cio.Crc32Plan(wl.packed_offsets(l3), l3) as p3:
@@ -384,9 +385,12 @@ def test_plan_workgroups(cuda, monkeypatch):
     l2 = wl.cfg2_lens()
     with cio.Crc32Plan(wl.packed_offsets(l2, align=16), l2) as p2:
         assert p2.workgroups == cus
-    l4 = np.full(8192, 4 << 20, np.uint64)      # uniform, 2 MiB per wave: one per CU
+    l4 = np.full(1024, 4 << 20, np.uint64)      # uniform, 1 MiB per wave: one per CU
     with cio.Crc32Plan(wl.packed_offsets(l4), l4) as p4:
         assert p4.workgroups == cus
+    l4 = np.full(8192, 4 << 20, np.uint64)      # cfg4 at one GPU, 8 MiB per wave: four
+    with cio.Crc32Plan(wl.packed_offsets(l4), l4) as p4:
+        assert p4.workgroups == 4 * cus
     monkeypatch.setenv("CIO_GPU_GRID", "17")
     with cio.Crc32Plan(wl.packed_offsets(l3), l3) as p3:
         assert p3.workgroups == 17

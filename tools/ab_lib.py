@@ -63,6 +63,7 @@ def main():
     for cfg in args.cfg.split(","):
         lens = {"cfg2": wl.cfg2_lens, "cfg3": wl.cfg3_lens,
                 "big": lambda: np.full(1024, 4 << 20, np.uint64),
+                "cfg4": lambda: np.full(8192, 4 << 20, np.uint64),
                 "mid": lambda: np.full(1024, 1638400, np.uint64),
                 "small": lambda: np.full(65536, 4096, np.uint64),
                 "cfg4k": lambda: np.full(102400, 4096, np.uint64)}[cfg]()
