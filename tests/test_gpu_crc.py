@@ -396,6 +396,23 @@ def test_plan_workgroups(cuda, monkeypatch):
         assert p3.workgroups == 17
 
 
+def test_read_stream_grids(cuda):
+    """The read-only ceiling kernel (bench.py's roofline.read_stream) on one
+    and four workgroups per CU and on a small grid; more than 4096
+    workgroups is refused with a message, nothing launched."""
+    import torch
+    lib = cio.lib()
+    buf = torch.zeros(64 << 20, dtype=torch.uint8, device=cuda)
+    s = torch.cuda.current_stream(cuda).cuda_stream
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    for wgs in (0, cus, 4 * cus, 3):
+        assert lib.cio_gpu_read_stream_grid(buf.data_ptr(), buf.numel(), wgs, s) == 0
+    assert lib.cio_gpu_read_stream(buf.data_ptr(), buf.numel(), s) == 0
+    torch.cuda.synchronize(cuda)
+    assert lib.cio_gpu_read_stream_grid(buf.data_ptr(), buf.numel(), 4097, s) != 0
+    assert b"4096" in lib.cio_gpu_last_error()
+
+
 def test_cfg4_shard_golden(cuda, golden):
     import torch
     g = golden["cfg4"]
