@@ -1570,6 +1570,45 @@ read_stream_kernel(const uint8_t *__restrict__ base, uint64_t S, uint32_t *__res
                 burn();
             }
         }
+    } else if (B & 0x80000000u) {
+        // diagnostic (CIO_GPU_RS_WGPOOL=k): the CRC kernel's split, but the
+        // last k steps of every wave's range form a workgroup pool that the
+        // workgroup's waves claim one step at a time (LDS atomic) once their
+        // own ranges are done: intra-workgroup balancing, priced on the
+        // read-only stream.
+        __shared__ uint32_t pool_next;
+        const uint32_t k = B & 0xffffu;
+        if (threadIdx.x == 0) {
+            pool_next = 0;
+        }
+        __syncthreads();
+        auto static_end = [&](uint64_t w, uint64_t &e1) {
+            const uint64_t a = wave_start(w, S, W), b = wave_start(w + 1, S, W);
+            e1 = b;
+            return b > a + k ? b - k : a;
+        };
+        uint64_t g1;
+        const uint64_t g0 = wave_start(wave, S, W), gs = static_end(wave, g1);
+        for (uint64_t g = g0; g < gs; ++g) {
+            step(g);
+        }
+        const uint32_t first = blockIdx.x * (kThreads / kWave);
+        for (;;) {
+            uint32_t item = 0;
+            if (lane == 0) {
+                item = atomicAdd(&pool_next, 1u);
+            }
+            item = __builtin_amdgcn_readfirstlane(item);
+            if (item >= (kThreads / kWave) * k) {
+                break;
+            }
+            uint64_t o1;
+            const uint64_t os = static_end(first + item / k, o1);
+            const uint64_t g = os + item % k;
+            if (g < o1) {
+                step(g);
+            }
+        }
     } else if (B == 0) {
         // the CRC kernel's split: one contiguous range per wave
         const uint64_t g0 = wave_start(wave, S, W), g1 = wave_start((uint64_t) wave + 1, S, W);
@@ -2399,6 +2438,12 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
     uint32_t B = 0;
     if (const char *r = getenv("CIO_GPU_RS_BLOCK")) {
         B = (uint32_t) atoi(r);
+    }
+    if (const char *r = getenv("CIO_GPU_RS_WGPOOL")) {
+        const int k = atoi(r);
+        if (k > 0 && k < 65536) {
+            B = 0x80000000u | (uint32_t) k;
+        }
     }
     unsigned long long *stamps = nullptr;
     if (const char *r = getenv("CIO_GPU_RS_STAMPS")) {
