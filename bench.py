@@ -1341,7 +1341,7 @@ def main():
             # that allocate and free tens of GB of HBM (cfg4: 34 GB, cfg3:
             # 40 GB): the driver clears freed VRAM in the background on the
             # SDMA engines the H2D copies use, which slows host batches by
-            # ~11% for ~1 s after such a free (profiles/r04/e2e_vram_free_*).
+            # ~11% for ~1 s after such a free (profiles/r04/e2e_vram_free/README.md).
             host_legs = other_configs(args, rank, world, device, dist, only=("e2e", "verify", "perf"))
             res["other_chunk_sizes"] = other_chunk_sizes(args, rank, world, device, dist)
             dev_legs = other_configs(args, rank, world, device, dist, only=("cfg3", "sha1"))
