@@ -20,7 +20,8 @@ EXPORTS = (
     "cio_gpu_init", "cio_gpu_last_error", "cio_gpu_version",
     "cio_crc32_shift", "cio_crc32_combine",
     "cio_crc32_plan_create", "cio_crc32_plan_destroy", "cio_crc32_plan_exec",
-    "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_plan_workgroups", "cio_crc32_batch_dev", "cio_crc32_batch_host",
+    "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_plan_workgroups", "cio_crc32_ring_create", "cio_crc32_ring_exec",
+    "cio_crc32_ring_join", "cio_crc32_ring_destroy", "cio_crc32_batch_dev", "cio_crc32_batch_host",
     "cio_crc32_batch_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device", "cio_gpu_numa_node",
     "cio_crc32_host_register", "cio_crc32_host_unregister", "cio_gpu_pipe_last_timing",
     "cio_crc32_cpu_max", "cio_crc32_set_cpu_max", "cio_crc32_host_threads", "cio_crc32_set_host_threads",
@@ -71,6 +72,11 @@ def _bind(lib):
         "cio_crc32_plan_bytes": (ctypes.c_uint64, [V]),
         "cio_crc32_plan_kernel": (ctypes.c_char_p, [V]),
         "cio_crc32_plan_workgroups": (ctypes.c_uint32, [V]),
+        "cio_crc32_ring_create": (ctypes.c_int, [ctypes.POINTER(V), ctypes.POINTER(ctypes.c_uint64),
+                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_int]),
+        "cio_crc32_ring_exec": (ctypes.c_int, [V, V, V, V, V]),
+        "cio_crc32_ring_join": (ctypes.c_int, [V, V]),
+        "cio_crc32_ring_destroy": (None, [V]),
         "cio_crc32_batch_dev": (ctypes.c_int, [V, c_u64_p, c_u64_p, V, V, ctypes.c_size_t, V]),
         "cio_crc32_batch_host": (ctypes.c_int, [P(V), P(ctypes.c_size_t), c_u32_p, c_u32_p,
                                                 ctypes.c_size_t]),

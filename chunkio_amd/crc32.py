@@ -137,6 +137,50 @@ class Crc32Plan:
         self.close()
 
 
+class Crc32Ring:
+    """`depth` plans of one geometry on their own streams (cio_crc32_ring_*):
+    exec() queues a batch behind the caller stream's earlier work without
+    making that stream wait for it, so consecutive batches overlap at their
+    kernel edges; join() makes the caller stream wait for every batch queued
+    so far (read the outputs after it)."""
+
+    def __init__(self, offs, lens, depth=2):
+        self._offs, po = _u64_array(offs)
+        self._lens, pl = _u64_array(lens)
+        if self._offs.shape != self._lens.shape:
+            raise ValueError("offs and lens must have the same length")
+        self.n = int(self._offs.size)
+        handle = ctypes.c_void_p()
+        _lib.check(_lib.lib().cio_crc32_ring_create(ctypes.byref(handle), po, pl, self.n, int(depth)),
+                   "cio_crc32_ring_create")
+        self._handle = handle
+
+    def exec(self, base, out, seeds=None, stream=None):
+        _lib.check(_lib.lib().cio_crc32_ring_exec(self._handle, _ptr(base), _ptr(seeds), _ptr(out),
+                                                  _stream_ptr(stream)),
+                   "cio_crc32_ring_exec")
+
+    def join(self, stream=None):
+        _lib.check(_lib.lib().cio_crc32_ring_join(self._handle, _stream_ptr(stream)), "cio_crc32_ring_join")
+
+    def close(self):
+        if getattr(self, "_handle", None):
+            _lib.lib().cio_crc32_ring_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def _to_u32_numpy(t):
     return t.cpu().numpy().view(np.uint32).copy()
 

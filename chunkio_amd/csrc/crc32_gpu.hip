@@ -2168,6 +2168,100 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     return CIO_OK;
 }
 
+/* A ring of `depth` plans of one geometry, each on its own stream (see the
+ * header): consecutive batches overlap at their kernel edges. */
+struct cio_crc32_ring {
+    std::vector<cio_crc32_plan *> plans;
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> ready, done;    // per slot: caller's inputs, slot's last batch
+    std::vector<bool> pending;              // slot has work the caller has not joined
+    unsigned next = 0;
+};
+
+void cio_crc32_ring_destroy(cio_crc32_ring *r)
+{
+    if (!r) {
+        return;
+    }
+    for (hipStream_t st : r->streams) {
+        if (st) (void) hipStreamSynchronize(st);
+    }
+    for (size_t i = 0; i < r->plans.size(); i++) {
+        cio_crc32_plan_destroy(r->plans[i]);
+        if (r->ready[i]) (void) hipEventDestroy(r->ready[i]);
+        if (r->done[i]) (void) hipEventDestroy(r->done[i]);
+        if (r->streams[i]) (void) hipStreamDestroy(r->streams[i]);
+    }
+    delete r;
+}
+
+int cio_crc32_ring_create(cio_crc32_ring **out, const uint64_t *offs, const uint64_t *lens, size_t n, int depth)
+{
+    if (!out) {
+        return fail("cio_crc32_ring_create: null argument");
+    }
+    *out = nullptr;
+    if (depth < 1 || depth > 8) {
+        return fail("cio_crc32_ring_create: depth must be 1..8");
+    }
+    cio_crc32_ring *r = new cio_crc32_ring();
+    r->plans.assign((size_t) depth, nullptr);
+    r->streams.assign((size_t) depth, nullptr);
+    r->ready.assign((size_t) depth, nullptr);
+    r->done.assign((size_t) depth, nullptr);
+    r->pending.assign((size_t) depth, false);
+    for (int i = 0; i < depth; i++) {
+        if (cio_crc32_plan_create(&r->plans[(size_t) i], offs, lens, n) != CIO_OK) {
+            cio_crc32_ring_destroy(r);
+            return CIO_ERROR;    // (the plan's message stands)
+        }
+        hipError_t e = hipStreamCreateWithFlags(&r->streams[(size_t) i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ready[(size_t) i], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&r->done[(size_t) i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            cio_crc32_ring_destroy(r);
+            return fail("cio_crc32_ring_create", e);
+        }
+    }
+    *out = r;
+    return CIO_OK;
+}
+
+int cio_crc32_ring_exec(cio_crc32_ring *r, const void *dev_base, const uint32_t *dev_seeds, uint32_t *dev_out,
+                        void *stream)
+{
+    if (!r) {
+        return fail("cio_crc32_ring_exec: null ring");
+    }
+    const size_t i = r->next++ % r->plans.size();
+    const hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
+    // the batch waits for everything the caller queued before it (its inputs);
+    // the slot's stream orders it after the slot's previous batch (scratch reuse)
+    HIP_TRY(hipEventRecord(r->ready[i], caller), "cio_crc32_ring_exec: hipEventRecord");
+    HIP_TRY(hipStreamWaitEvent(r->streams[i], r->ready[i], 0), "cio_crc32_ring_exec: hipStreamWaitEvent");
+    if (plan_exec_impl(r->plans[i], dev_base, dev_seeds, dev_out, nullptr, r->streams[i]) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    HIP_TRY(hipEventRecord(r->done[i], r->streams[i]), "cio_crc32_ring_exec: hipEventRecord");
+    r->pending[i] = true;
+    return CIO_OK;
+}
+
+int cio_crc32_ring_join(cio_crc32_ring *r, void *stream)
+{
+    if (!r) {
+        return fail("cio_crc32_ring_join: null ring");
+    }
+    const hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
+    for (size_t i = 0; i < r->plans.size(); i++) {
+        if (r->pending[i]) {
+            HIP_TRY(hipStreamWaitEvent(caller, r->done[i], 0), "cio_crc32_ring_join: hipStreamWaitEvent");
+            r->pending[i] = false;
+        }
+    }
+    return CIO_OK;
+}
+
 /* Test hook (not in the public header; host only, no device): the plan's
  * work split for W waves.  Per chunk: w0, w1, npieces (3 words); per wave:
  * the LDS-fold flags.  Returns 0, or -1 on a plan error. */

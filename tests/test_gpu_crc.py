@@ -413,6 +413,46 @@ def test_read_stream_grids(cuda):
     assert b"4096" in lib.cio_gpu_last_error()
 
 
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_ring_batches_overlap_same_results(cuda, depth):
+    """cio_crc32_ring: batches queued on `depth` plans with their own streams,
+    joined on the caller's stream, give every batch's CRCs (seeded and not),
+    the same as one plan batch by batch; the batch queued after a caller-side
+    write sees that write; depth outside 1..8 is refused."""
+    import torch
+    rng = np.random.default_rng(depth)
+    lens = np.full(200, 409600, np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    total = wl.batch_bytes(offs, lens)
+    bufs = [torch.empty(total + 64, dtype=torch.uint8, device=cuda) for _ in range(5)]
+    for b, t in enumerate(bufs):
+        cio.fill_synthetic(t, offs, lens, 0x5EED + b)
+    seeds_np = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+    seeds = torch.from_numpy(seeds_np.view(np.int32)).to(cuda)
+    outs = [torch.empty(len(lens), dtype=torch.int32, device=cuda) for _ in range(10)]
+    with cio.Crc32Ring(offs, lens, depth=depth) as ring:
+        for k in range(10):
+            if k == 7:
+                bufs[k % 5][int(offs[3]) + 5] ^= 0xFF      # a caller-side write the next batch must see
+            ring.exec(bufs[k % 5], outs[k], seeds=seeds if k % 2 else None)
+        ring.join()
+    torch.cuda.synchronize(cuda)
+    with cio.Crc32Plan(offs, lens) as plan:
+        for k in range(10):
+            want = torch.empty_like(outs[k])
+            plan.exec(bufs[k % 5], want, seeds=seeds if k % 2 else None)
+            torch.cuda.synchronize(cuda)
+            if k < 7 and k % 5 == 2:
+                continue    # batch 2's buffer was changed after it ran
+            assert torch.equal(outs[k], want), k
+    host = bufs[2].cpu().numpy()
+    assert int(outs[7].cpu().numpy().view(np.uint32)[3]) == po.crc_batch(host, offs[3:4], lens[3:4],
+                                                                          seeds=seeds_np[3:4])[0]
+    for bad in (0, 9):
+        with pytest.raises(cio.CioGpuError):
+            cio.Crc32Ring(offs, lens, depth=bad)
+
+
 def test_cfg4_shard_golden(cuda, golden):
     import torch
     g = golden["cfg4"]
