@@ -256,6 +256,20 @@ def crc32_batch_host_packed(host, offs, lens, seeds=None, devices=None):
     return out[:n]
 
 
+def crc32_split_host(buf, seed=CRC_INIT, devices=None):
+    """Raw crc_update(seed, buf) of ONE host buffer split over `devices`
+    (cio_crc32_split_host_multi: a piece per device, joined with
+    cio_crc32_combine)."""
+    arr = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    out = ctypes.c_uint32(0)
+    devs = (ctypes.c_int * len(devices))(*devices) if devices else None
+    _lib.check(_lib.lib().cio_crc32_split_host_multi(arr.ctypes.data if arr.size else None, arr.size,
+                                                     seed & 0xFFFFFFFF, ctypes.byref(out), devs,
+                                                     len(devices) if devices else 0),
+               "cio_crc32_split_host_multi")
+    return int(out.value)
+
+
 def crc32_batch_cpu_packed(host, offs, lens, seeds=None, threads=1):
     """The same batch as crc32_batch_host_packed on the host CPU
     (cio_crc32_batch_cpu: the library's crc_update on `threads` threads)."""

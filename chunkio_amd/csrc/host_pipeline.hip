@@ -1088,6 +1088,41 @@ extern "C" int cio_crc32_batch_host_multi(const void *const *bufs, const size_t 
                        "cio_crc32_batch_host_multi");
 }
 
+extern "C" int cio_crc32_split_host_multi(const void *buf, size_t len, uint32_t seed, uint32_t *out_raw,
+                                          const int *devices, int ndev)
+{
+    if (!out_raw || (len && !buf) || (ndev > 0 && !devices)) {
+        return fail("cio_crc32_split_host_multi: null argument");
+    }
+    if (len == 0) {
+        *out_raw = seed;
+        return CIO_OK;
+    }
+    const size_t G = ndev > 0 ? (size_t) ndev : 1;
+    // pieces of a 4 KiB multiple (whole wave-steps on each device), the last short
+    const size_t piece = std::max<size_t>(4096, ((len + G - 1) / G + 4095) & ~(size_t) 4095);
+    std::vector<const void *> bufs;
+    std::vector<size_t> lens;
+    std::vector<uint32_t> seeds, out;
+    for (size_t at = 0; at < len; at += piece) {
+        bufs.push_back(static_cast<const uint8_t *>(buf) + at);
+        lens.push_back(std::min(piece, len - at));
+        seeds.push_back(at == 0 ? seed : 0u);
+    }
+    out.resize(bufs.size());
+    const int rc = cio_crc32_batch_host_multi(bufs.data(), lens.data(), seeds.data(), out.data(), bufs.size(),
+                                              ndev > 0 ? devices : nullptr, ndev > 0 ? (int) std::min(G, bufs.size()) : 0);
+    if (rc != CIO_OK) {
+        return rc;
+    }
+    uint32_t acc = out[0];
+    for (size_t i = 1; i < out.size(); i++) {
+        acc = cio_crc32_combine(acc, out[i], lens[i]);
+    }
+    *out_raw = acc;
+    return CIO_OK;
+}
+
 /* Diagnostic (not in the public header): the H2D DMA rate from `host`
  * (pinned, registered or pageable) into a device buffer, `reps` copies of
  * `bytes` on one stream; GB/s, or a negative value on error.  bench.py puts

@@ -170,6 +170,15 @@ int  cio_crc32_batch_host_multi(const void *const *bufs, const size_t *lens,
                                 const uint32_t *seeds, uint32_t *out_raw, size_t n,
                                 const int *devices, int ndev);
 
+/* ONE host buffer split over several GPUs (SURVEY §8(e)'s optional case):
+ * its len bytes are cut into ndev pieces (4 KiB multiples), piece i CRC'd on
+ * devices[i] (the first seeded with `seed`, the others from 0) through
+ * cio_crc32_batch_host_multi, and the piece states joined on the host with
+ * cio_crc32_combine: *out_raw = crc_update(seed, buf, len).  The only
+ * combine step the path has; no collective. */
+int  cio_crc32_split_host_multi(const void *buf, size_t len, uint32_t seed, uint32_t *out_raw,
+                                const int *devices, int ndev);
+
 /* The same over file ranges: chunk i is bytes [foffs[i], foffs[i] + lens[i])
  * of the open file fds[i], read by the pipeline's copy threads with pread()
  * straight into pinned staging (no mapping).  For batch verifies of chunk

@@ -453,6 +453,21 @@ def test_ring_batches_overlap_same_results(cuda, depth):
             cio.Crc32Ring(offs, lens, depth=bad)
 
 
+@pytest.mark.parametrize("ndev", [1, 2, 3, 8])
+def test_split_one_buffer_over_devices(cuda, ndev):
+    """cio_crc32_split_host_multi: one buffer cut into a piece per (logical)
+    device, the piece states joined with cio_crc32_combine, equals crc_update
+    over the whole buffer, seeded or not; lengths below one piece per device,
+    not a 4 KiB multiple, and empty."""
+    rng = np.random.default_rng(ndev)
+    for ln in (0, 1, 4095, 4096 * ndev + 7, 3 << 20, (64 << 20) + 12345):
+        buf = rng.integers(0, 256, ln, dtype=np.uint8)
+        for seed in (cio.CRC_INIT, 0x1234ABCD):
+            want = po.crc_batch(buf, np.zeros(1, np.uint64), np.full(1, ln, np.uint64),
+                                seeds=np.full(1, seed, np.uint32))[0]
+            assert cio.crc32_split_host(buf, seed, devices=[0] * ndev) == want, (ln, seed)
+
+
 def test_cfg4_shard_golden(cuda, golden):
     import torch
     g = golden["cfg4"]
