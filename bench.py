@@ -154,6 +154,26 @@ def gather_over_ranks(x, dist, device):
     return [float(v.item()) for v in out]
 
 
+def job_digest_matches(local, n_total, want_sha256, dist):
+    """A strong-scaled job checked whole at any N: every rank's raw CRCs (its
+    round-robin shard, in shard order) gathered to rank 0 in job order -- 4
+    bytes per chunk over gloo, after the timed region, not on the data path --
+    and the SHA-256 of the job's little-endian u32 array compared with
+    `want_sha256`.  True/False on rank 0, None on the others."""
+    import hashlib
+    local = np.asarray(local, dtype=np.uint32)
+    if dist is None:
+        job = local
+    else:
+        from chunkio_amd import shard
+        job = shard.gather_results(local, n_total, dst=0)
+        if job is None:
+            return None
+    if len(job) != n_total:
+        return False
+    return hashlib.sha256(job.astype("<u4").tobytes()).hexdigest() == want_sha256
+
+
 def geometry(cfg, rank, world):
     """(lens, ids, seed, workload description, scaling) of this rank's shard."""
     from chunkio_amd import workloads as wl
@@ -483,6 +503,14 @@ def run_crc(args, rank, world, device, dist):
             g = json.load(f)["cfg3"]
         check["golden_sha256_match_all_chunks"] = hashlib.sha256(gpu0.astype("<u4").tobytes()).hexdigest() == \
             g["sha256_of_raw_le"]
+    if args.config == "cfg4":
+        # The whole 8192-chunk job at every N: each rank's shard gathered to
+        # rank 0 in job order against the reference crc32.c's digest.
+        with open(os.path.join(ROOT, "tests", "golden", "crc32_vectors.json")) as f:
+            g = json.load(f)["cfg4"]
+        m = job_digest_matches(gpu0, wl.CFG4_N, g["sha256_of_raw_le"], dist)
+        if rank == 0:
+            check["golden_sha256_match_full_job"] = bool(m)
     if args.config in ("cfg3", "cfg4"):
         # Full-size batches: 8 chunks spread over the batch (first, last and
         # evenly between), device bytes copied back and CRC'd with zlib.

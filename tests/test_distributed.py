@@ -297,3 +297,50 @@ def test_bench_pg_timeout_bounds_a_barrier_without_the_launcher():
     assert procs[1].returncode == 1
     assert procs[0].returncode != 0
     assert time.monotonic() - t0 < 60
+
+
+def _job_digest_worker(rank, world, port, want, q):
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 37
+        job = (np.arange(n, dtype=np.uint64) * 0x9E3779B1 % (1 << 32)).astype(np.uint32)
+        local = job[shard.shard_ids(n, rank, world)]
+        ok = bench.job_digest_matches(local, n, want, dist)
+        bad = local.copy()
+        if rank == world - 1:
+            bad[-1] ^= 1
+        nok = bench.job_digest_matches(bad, n, want, dist)
+        if rank == 0:
+            q.put((ok, nok))
+        else:
+            assert ok is None and nok is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_job_digest_gathers_shards(world):
+    """bench.py's full-job check of cfg4 at N > 1: every rank's round-robin
+    shard gathered to rank 0 in job order; one flipped bit on the last rank
+    fails it."""
+    import hashlib
+    import bench
+    n = 37
+    job = (np.arange(n, dtype=np.uint64) * 0x9E3779B1 % (1 << 32)).astype(np.uint32)
+    want = hashlib.sha256(job.astype("<u4").tobytes()).hexdigest()
+    assert bench.job_digest_matches(job, n, want, None) is True
+    assert bench.job_digest_matches(job[:-1], n, want, None) is False
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_job_digest_worker, args=(r, world, port, want, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, nok = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert ok is True and nok is False
