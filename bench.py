@@ -155,23 +155,33 @@ def gather_over_ranks(x, dist, device):
 
 
 def job_digest_matches(local, n_total, want_sha256, dist):
-    """A strong-scaled job checked whole at any N: every rank's raw CRCs (its
-    round-robin shard, in shard order) gathered to rank 0 in job order -- 4
-    bytes per chunk over gloo, after the timed region, not on the data path --
-    and the SHA-256 of the job's little-endian u32 array compared with
-    `want_sha256`.  True/False on rank 0, None on the others."""
+    """A job checked whole at any N: every rank's results (its round-robin
+    shard, in shard order: raw u32 CRCs, or (n, 20) uint8 SHA-1 digests) are
+    gathered to rank 0 in job order -- 4 bytes per word over gloo, after the
+    timed region, not on the data path -- and the SHA-256 of the job's bytes
+    (u32 little-endian / digests concatenated) compared with `want_sha256`.
+    True/False on rank 0, None on the others."""
     import hashlib
-    local = np.asarray(local, dtype=np.uint32)
+    local = np.ascontiguousarray(local)
+    words = local.astype(np.uint32)[:, None] if local.ndim == 1 else local.view("<u4")
     if dist is None:
-        job = local
+        job = words
     else:
         from chunkio_amd import shard
-        job = shard.gather_results(local, n_total, dst=0)
-        if job is None:
+        cols = [shard.gather_results(words[:, k], n_total, dst=0) for k in range(words.shape[1])]
+        if cols[0] is None:
             return None
+        job = np.stack(cols, axis=1)
     if len(job) != n_total:
         return False
     return hashlib.sha256(job.astype("<u4").tobytes()).hexdigest() == want_sha256
+
+
+def weak_job_golden(cfg, world):
+    """SHA-256 of the weak-scaled `cfg` job at `world` GPUs, or None if the
+    fixture has none (tests/golden/make_golden.py weak_jobs: N = 1..8)."""
+    with open(os.path.join(ROOT, "tests", "golden", "crc32_vectors.json")) as f:
+        return json.load(f).get("weak_jobs", {}).get(cfg, {}).get(str(world))
 
 
 def geometry(cfg, rank, world):
@@ -503,6 +513,15 @@ def run_crc(args, rank, world, device, dist):
             g = json.load(f)["cfg3"]
         check["golden_sha256_match_all_chunks"] = hashlib.sha256(gpu0.astype("<u4").tobytes()).hexdigest() == \
             g["sha256_of_raw_le"]
+    if args.config in ("cfg2", "cfg4k", "cfg3"):
+        # The whole weak job at every N <= 8 (N x the per-GPU batch): each
+        # rank's shard gathered to rank 0 in job order against the reference
+        # crc32.c's digest of that job.
+        want = weak_job_golden(args.config, world)
+        if want is not None:
+            m = job_digest_matches(gpu0, len(lens) * world, want, dist)
+            if rank == 0:
+                check["golden_sha256_match_full_job"] = bool(m)
     if args.config == "cfg4":
         # The whole 8192-chunk job at every N: each rank's shard gathered to
         # rank 0 in job order against the reference crc32.c's digest.
@@ -617,6 +636,12 @@ def run_sha1(args, rank, world, device, dist):
         bytes(got[i]) == hashlib.sha1(wl.gen_chunk(seed, int(ids[i]) if ids is not None else i,
                                                    int(lens[i])).tobytes()).digest() for i in sample),
              "sample_chunks": sample}
+    want = weak_job_golden("sha1", world)
+    if want is not None:
+        # every digest of the N-GPU job against hashlib's, gathered to rank 0
+        m = job_digest_matches(got, len(lens) * world, want, dist)
+        if rank == 0:
+            check["golden_sha256_match_full_job"] = bool(m)
     if world == 1:
         # all 1,024 digests against hashlib's (tests/golden/make_golden.py)
         with open(os.path.join(ROOT, "tests", "golden", "crc32_vectors.json")) as f:

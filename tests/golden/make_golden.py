@@ -8,7 +8,7 @@ reference's own fixture tests/data/400kb.txt (copied here as data), or the
 deterministic splitmix64 generator of chunkio_amd/workloads.py (parameters
 stored, not bytes).
 
-Run from the repo root:  python tests/golden/make_golden.py
+Run from the repo root:  python tests/golden/make_golden.py [--jobs-only]
 """
 import hashlib
 import json
@@ -56,9 +56,63 @@ def _cfg5_digest(i):
     return hashlib.sha1(wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes()).digest()
 
 
+# Weak-scaled jobs at N GPUs (bench.py --gpus N): chunk ids 0 .. N*n-1 of the
+# config, rank r owning ids r, r+N, ...  Chunk i's bytes and length depend on i
+# only, so the N-GPU job is the first N*n chunks of the 8-GPU one and one pass
+# over 8*n chunks pins every N = 1..8 by prefix digests.
+MAX_GPUS = 8
+_L3J = None
+
+
+def _cfg2_raw(i):
+    return ref_raw(INIT, wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes())
+
+
+def _cfg4k_raw(i):
+    return ref_raw(INIT, wl.gen_chunk(wl.CFG4K_SEED, i, wl.CFG4K_LEN).tobytes())
+
+
+def _cfg3_raw_job(i):
+    global _L3J
+    if _L3J is None:
+        _L3J = wl.cfg3_lens(MAX_GPUS * wl.CFG3_N)
+    return ref_raw(INIT, wl.gen_chunk(wl.CFG3_SEED, i, int(_L3J[i])).tobytes())
+
+
+def weak_jobs():
+    """SHA-256 of the raw CRCs (SHA-1 digests for sha1) of the N-GPU job, in
+    job order, for N = 1..8."""
+    out = {"note": "bench.py weak configs at N GPUs: ids 0..N*n-1 (rank r owns r, r+N, ...); "
+                   "sha256 of the job's raw CRCs as little-endian u32 (sha1: of the concatenated "
+                   "20-byte digests); ids past n use the same generator (chunkio_amd/workloads.py)"}
+    jobs = (("cfg2", _cfg2_raw, wl.CFG2_N, 32), ("cfg4k", _cfg4k_raw, wl.CFG4K_N, 4096),
+            ("cfg3", _cfg3_raw_job, wl.CFG3_N, 256))
+    for name, fn, n, cs in jobs:
+        with multiprocessing.Pool(7) as pool:
+            raw = np.asarray(pool.map(fn, range(MAX_GPUS * n), chunksize=cs), np.uint32)
+        out[name] = {str(g): hashlib.sha256(raw[: g * n].astype("<u4").tobytes()).hexdigest()
+                     for g in range(1, MAX_GPUS + 1)}
+        print(name, "done", flush=True)
+    with multiprocessing.Pool(7) as pool:
+        dg = pool.map(_cfg5_digest, range(MAX_GPUS * wl.CFG2_N), chunksize=32)
+    out["sha1"] = {str(g): hashlib.sha256(b"".join(dg[: g * wl.CFG2_N])).hexdigest()
+                   for g in range(1, MAX_GPUS + 1)}
+    return out
+
+
 def main():
     if pyoracle.ref() is None:
         sys.exit("oracle/_ref/libcrc32_ref.so missing: run `make -C oracle` with /root/reference present")
+    path = os.path.join(HERE, "crc32_vectors.json")
+    if "--jobs-only" in sys.argv:
+        # refresh only the weak-job digests of an existing fixture
+        with open(path) as f:
+            out = json.load(f)
+        out["weak_jobs"] = weak_jobs()
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        print("wrote", path)
+        return
     out = {"generator": "tests/golden/make_golden.py",
            "crc_model": "CRC-32/IEEE reflected 0xEDB88320; values are RAW crc_update states "
                         "(seed in, un-finalized out); finalized = raw ^ 0xffffffff"}
@@ -137,7 +191,8 @@ def main():
                    "cfg5_n": wl.CFG2_N,
                    "cfg5_sha256_of_digests": hashlib.sha256(b"".join(c5)).hexdigest(),
                    "400kb": hashlib.sha1(D400).hexdigest()}
-    with open(os.path.join(HERE, "crc32_vectors.json"), "w") as f:
+    out["weak_jobs"] = weak_jobs()
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", os.path.join(HERE, "crc32_vectors.json"))
 

@@ -299,7 +299,7 @@ def test_bench_pg_timeout_bounds_a_barrier_without_the_launcher():
     assert time.monotonic() - t0 < 60
 
 
-def _job_digest_worker(rank, world, port, want, q):
+def _job_digest_worker(rank, world, port, want, want_rows, q):
     import torch.distributed as dist
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -313,19 +313,21 @@ def _job_digest_worker(rank, world, port, want, q):
         if rank == world - 1:
             bad[-1] ^= 1
         nok = bench.job_digest_matches(bad, n, want, dist)
+        rows = np.random.default_rng(5).integers(0, 256, (n, 20), dtype=np.uint8)
+        rok = bench.job_digest_matches(rows[shard.shard_ids(n, rank, world)], n, want_rows, dist)
         if rank == 0:
-            q.put((ok, nok))
+            q.put((ok, nok, rok))
         else:
-            assert ok is None and nok is None
+            assert ok is None and nok is None and rok is None
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_job_digest_gathers_shards(world):
-    """bench.py's full-job check of cfg4 at N > 1: every rank's round-robin
-    shard gathered to rank 0 in job order; one flipped bit on the last rank
-    fails it."""
+    """bench.py's full-job check at N > 1: every rank's round-robin shard
+    (u32 CRCs, or 20-byte SHA-1 digests) gathered to rank 0 in job order; one
+    flipped bit on the last rank fails it."""
     import hashlib
     import bench
     n = 37
@@ -333,14 +335,18 @@ def test_bench_job_digest_gathers_shards(world):
     want = hashlib.sha256(job.astype("<u4").tobytes()).hexdigest()
     assert bench.job_digest_matches(job, n, want, None) is True
     assert bench.job_digest_matches(job[:-1], n, want, None) is False
+    rows = np.random.default_rng(5).integers(0, 256, (n, 20), dtype=np.uint8)
+    want_rows = hashlib.sha256(rows.tobytes()).hexdigest()
+    assert bench.job_digest_matches(rows, n, want_rows, None) is True
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_job_digest_worker, args=(r, world, port, want, q)) for r in range(world)]
+    procs = [ctx.Process(target=_job_digest_worker, args=(r, world, port, want, want_rows, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    ok, nok = q.get(timeout=120)
+    ok, nok, rok = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert ok is True and nok is False
+    assert ok is True and nok is False and rok is True

@@ -508,6 +508,48 @@ def test_cfg4_full_job_sharded_g1_2_4_8(cuda, golden):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4k", "cfg3", "sha1"])
+def test_weak_jobs_sharded_g2_8(cuda, golden, cfg):
+    """The weak-scaled jobs bench.py --gpus N runs (N x the per-GPU batch,
+    chunk i on rank i mod N) at N = 2 and 8, every rank's shard built exactly
+    as bench.geometry builds it and run one after another on this GPU; the
+    gathered job must equal the reference digest of that job
+    (tests/golden/make_golden.py weak_jobs: crc32.c + zlib, hashlib for SHA-1).
+    cfg3 at N = 8 is 318 GB of chunks, 40 GB at a time."""
+    import torch
+    import bench
+    from chunkio_amd import shard
+    from chunkio_amd import workloads as wl
+    dev = None
+    for world in (2, 8):
+        parts = []
+        for r in range(world):
+            lens, ids, seed, _, scaling = bench.geometry(cfg, r, world)
+            assert scaling == "weak"
+            offs = wl.packed_offsets(lens, align=16)
+            need = wl.batch_bytes(offs, lens) + 64
+            if dev is None or dev.numel() < need:
+                dev = None
+                torch.cuda.empty_cache()
+                dev = torch.empty(need, dtype=torch.uint8, device=cuda)
+            cio.fill_synthetic(dev, offs, lens, seed, ids=ids)
+            if cfg == "sha1":
+                parts.append(cio.sha1_batch_dev(dev, offs, lens).reshape(-1, 20))
+            else:
+                parts.append(cio.crc32_batch_dev(dev, offs, lens))
+        n = sum(len(p) for p in parts)
+        if cfg == "sha1":
+            job = np.empty((n, 20), np.uint8)
+            for r, p in enumerate(parts):
+                job[shard.shard_ids(n, r, world)] = p
+            got = hashlib.sha256(job.tobytes()).hexdigest()
+        else:
+            got = hashlib.sha256(shard.assemble(n, world, parts).astype("<u4").tobytes()).hexdigest()
+        assert got == golden["weak_jobs"][cfg][str(world)], (cfg, world)
+    del dev
+    torch.cuda.empty_cache()
+
+
 def test_host_batch_end_to_end(cuda, data400):
     rng = np.random.default_rng(10)
     bufs = [np.frombuffer(b"\0\0" + data400, np.uint8)]

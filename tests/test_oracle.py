@@ -145,3 +145,23 @@ def test_cfg3_fixture_samples_and_digest_shape(golden):
     for i, raw in list(zip(g["sample_idx"], g["sample_raw"]))[::8]:
         assert zlib.crc32(wl.gen_chunk(g["seed"], i, int(l3[i])).tobytes()) ^ 0xFFFFFFFF == raw
     assert len(g["sha256_of_raw_le"]) == 64
+
+
+def test_weak_job_fixtures(golden):
+    """The weak-job digests (bench.py --gpus N, N = 1..8) agree at N = 1 with
+    the per-config fixtures made by the separate full-batch passes, cfg2's
+    N = 2 job is recomputed here with zlib, and cfg3's lengths are a prefix-
+    stable function of the chunk id (the N-GPU job is the first N x 65 536)."""
+    import hashlib
+    import zlib
+    j = golden["weak_jobs"]
+    assert j["cfg2"]["1"] == golden["cfg2"]["sha256_of_raw_le"]
+    assert j["cfg3"]["1"] == golden["cfg3"]["sha256_of_raw_le"]
+    assert j["sha1"]["1"] == golden["sha1"]["cfg5_sha256_of_digests"]
+    for k in ("cfg2", "cfg4k", "cfg3", "sha1"):
+        assert sorted(j[k], key=int) == [str(g) for g in range(1, 9)]
+        assert len(set(j[k].values())) == 8
+    c2 = np.asarray([zlib.crc32(wl.gen_chunk(wl.CFG2_SEED, i, wl.CFG2_LEN).tobytes()) ^ 0xFFFFFFFF
+                     for i in range(2 * wl.CFG2_N)], np.uint32)
+    assert hashlib.sha256(c2.astype("<u4").tobytes()).hexdigest() == j["cfg2"]["2"]
+    np.testing.assert_array_equal(wl.cfg3_lens(8 * wl.CFG3_N)[: wl.CFG3_N], wl.cfg3_lens())
