@@ -1194,7 +1194,8 @@ def other_chunk_sizes(args, rank, world, device, dist):
         out[cfg] = {"value": r["value"], "unit": r["unit"], "scaling": r["scaling"], "steps": steps,
                     "warmup": warm, "ms_per_step": r["ms_per_step"], "workload": r["config"]["workload"],
                     "roofline": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "kernel",
-                                                                "kernel_ms_mean", "traffic")},
+                                                                "kernel_ms_mean", "traffic", "workgroups",
+                                                                "frac_of_read_stream")},
                     "check": r.get("check", {})}
         if "cpu_baseline" in r:
             out[cfg]["cpu_baseline"] = r["cpu_baseline"]
