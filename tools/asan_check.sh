@@ -5,6 +5,8 @@
 #   bash tools/asan_check.sh host       # the C replays on the host CRC route
 #   bash tools/asan_check.sh gpu        # the same replays with every verify /
 #                                       # sync on the GPU route (host pipeline)
+#   bash tools/asan_check.sh tsan       # here: ThreadSanitizer build + the host
+#                                       # route on the 8-thread CRC pool
 #
 # Every host source of libchunkio_amd.so is instrumented: the C files with
 # clang, and the host side of the .hip files (each -fsanitize= after
@@ -69,8 +71,32 @@ host|gpu)
     fi
     echo "asan $MODE: clean"
     ;;
+tsan)
+    # Same sources with -fsanitize=thread (host code only), into build/tsan;
+    # the host CRC pool (8 threads) and the 16-thread verify opens.
+    T=build/tsan
+    mkdir -p $T/bin
+    for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch; do
+        $CL -O1 -g -fPIC -std=gnu11 -fsanitize=thread $INC -c -o $T/$f.o chunkio_amd/csrc/$f.c
+    done
+    for f in crc32_gpu host_pipeline sha1_gpu; do
+        $HIPCC -O1 -g -fPIC --offload-arch=gfx950 -std=c++17 $INC -munsafe-fp-atomics \
+            -mllvm -amdgpu-kernarg-preload-count=9 -Xarch_host -fsanitize=thread -c -o $T/$f.o chunkio_amd/csrc/$f.hip
+    done
+    $HIPCC -shared -fPIC --offload-arch=gfx950 -o $T/libchunkio_amd.so $T/*.o -lpthread
+    $CL -O1 -g -std=gnu11 -fsanitize=thread -Iinclude -o $T/bin/test_chunk_api tests/c/test_chunk_api.c \
+        -L$T -lchunkio_amd -Wl,-rpath,"$PWD/$T"
+    W=$(mktemp -d /tmp/cioa-tsan-XXXXXX)
+    trap 'rm -rf "$W"' EXIT
+    export TSAN_OPTIONS=halt_on_error=1
+    for m in immediate deferred; do
+        CIOA_CPU_CRC_MAX=$((1 << 62)) CIOA_HOST_CRC_THREADS=8 \
+            timeout -k 10 900 $T/bin/test_chunk_api tests/golden/400kb.txt "$W" $m | tail -1
+    done
+    echo "tsan host: clean"
+    ;;
 *)
-    echo "usage: $0 build|host|gpu" >&2
+    echo "usage: $0 build|host|gpu|tsan" >&2
     exit 2
     ;;
 esac
