@@ -7,6 +7,7 @@
 #                                       # sync on the GPU route (host pipeline)
 #   bash tools/asan_check.sh tsan       # here: ThreadSanitizer build + the host
 #                                       # route on the 8-thread CRC pool
+#   bash tools/asan_check.sh tsan-gpu   # that build's replay on the GPU route
 #
 # Every host source of libchunkio_amd.so is instrumented: the C files with
 # clang, and the host side of the .hip files (each -fsanitize= after
@@ -71,32 +72,44 @@ host|gpu)
     fi
     echo "asan $MODE: clean"
     ;;
-tsan)
-    # Same sources with -fsanitize=thread (host code only), into build/tsan;
-    # the host CRC pool (8 threads) and the 16-thread verify opens.
+tsan|tsan-gpu)
+    # Same sources with -fsanitize=thread (host code only): objects in
+    # build/tsan, library and replay in chunkio_amd/lib/tsan, tests/c/bin/tsan
+    # (so a GPU box gets them).  tsan builds and runs the host route on the
+    # 8-thread CRC pool; tsan-gpu runs the prebuilt replay on the GPU route.
     T=build/tsan
-    mkdir -p $T/bin
-    for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch; do
-        $CL -O1 -g -fPIC -std=gnu11 -fsanitize=thread $INC -c -o $T/$f.o chunkio_amd/csrc/$f.c
-    done
-    for f in crc32_gpu host_pipeline sha1_gpu; do
-        $HIPCC -O1 -g -fPIC --offload-arch=gfx950 -std=c++17 $INC -munsafe-fp-atomics \
-            -mllvm -amdgpu-kernarg-preload-count=9 -Xarch_host -fsanitize=thread -c -o $T/$f.o chunkio_amd/csrc/$f.hip
-    done
-    $HIPCC -shared -fPIC --offload-arch=gfx950 -o $T/libchunkio_amd.so $T/*.o -lpthread
-    $CL -O1 -g -std=gnu11 -fsanitize=thread -Iinclude -o $T/bin/test_chunk_api tests/c/test_chunk_api.c \
-        -L$T -lchunkio_amd -Wl,-rpath,"$PWD/$T"
+    TL=chunkio_amd/lib/tsan
+    TB=tests/c/bin/tsan
+    if [ "$MODE" = tsan ]; then
+        mkdir -p $T $TL $TB
+        for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch; do
+            $CL -O1 -g -fPIC -std=gnu11 -fsanitize=thread $INC -c -o $T/$f.o chunkio_amd/csrc/$f.c
+        done
+        for f in crc32_gpu host_pipeline sha1_gpu; do
+            $HIPCC -O3 -g -fPIC --offload-arch=gfx950 -std=c++17 $INC -munsafe-fp-atomics \
+                -mllvm -amdgpu-atomic-optimizer-strategy=None -mllvm -amdgpu-kernarg-preload-count=9 \
+                -Xarch_host -fsanitize=thread -c -o $T/$f.o chunkio_amd/csrc/$f.hip
+        done
+        $HIPCC -shared -fPIC --offload-arch=gfx950 -o $TL/libchunkio_amd.so $T/*.o -lpthread
+        $CL -O1 -g -std=gnu11 -fsanitize=thread -Iinclude -o $TB/test_chunk_api tests/c/test_chunk_api.c \
+            -L$TL -lchunkio_amd -Wl,-rpath,'$ORIGIN/../../../../chunkio_amd/lib/tsan'
+    fi
     W=$(mktemp -d /tmp/cioa-tsan-XXXXXX)
     trap 'rm -rf "$W"' EXIT
     export TSAN_OPTIONS=halt_on_error=1
     for m in immediate deferred; do
-        CIOA_CPU_CRC_MAX=$((1 << 62)) CIOA_HOST_CRC_THREADS=8 \
-            timeout -k 10 900 $T/bin/test_chunk_api tests/golden/400kb.txt "$W" $m | tail -1
+        if [ "$MODE" = tsan ]; then
+            CIOA_CPU_CRC_MAX=$((1 << 62)) CIOA_HOST_CRC_THREADS=8 \
+                timeout -k 10 900 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m | tail -1
+        else
+            TSAN_OPTIONS=halt_on_error=1:suppressions=$PWD/tools/tsan_rocm.supp CIOA_CPU_CRC_MAX=0 \
+                timeout -k 10 300 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m
+        fi
     done
-    echo "tsan host: clean"
+    echo "$MODE: clean"
     ;;
 *)
-    echo "usage: $0 build|host|gpu|tsan" >&2
+    echo "usage: $0 build|host|gpu|tsan|tsan-gpu" >&2
     exit 2
     ;;
 esac
