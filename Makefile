@@ -19,7 +19,7 @@ HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/host_pipeline.o $(BLD)/sha1_gpu.o
 
 CTEST   := tests/c/bin
 REF_INC := /root/reference/include/chunkio/cio_crc32.h
-CTESTS  := $(CTEST)/test_crc32_dropin $(CTEST)/test_chunk_api $(if $(wildcard $(REF_INC)),$(CTEST)/test_crc32_dropin_ref)
+CTESTS  := $(CTEST)/test_crc32_dropin $(CTEST)/test_chunk_api $(CTEST)/test_multi $(if $(wildcard $(REF_INC)),$(CTEST)/test_crc32_dropin_ref)
 CLINK   := -Lchunkio_amd/lib -lchunkio_amd -Wl,-rpath,'$$ORIGIN/../../../chunkio_amd/lib'
 
 all: $(LIB) oracle ctests
@@ -40,6 +40,10 @@ $(CTEST)/test_crc32_dropin_ref: tests/c/test_crc32_dropin.c $(LIB) include/crc32
 $(CTEST)/test_chunk_api: tests/c/test_chunk_api.c $(LIB) $(wildcard include/*/*.h)
 	@mkdir -p $(CTEST)
 	$(CC) -O2 -Wall -Wextra -std=gnu11 -Iinclude -o $@ $< $(CLINK)
+
+$(CTEST)/test_multi: tests/c/test_multi.c $(LIB) include/chunkio_amd/cio_crc32_gpu.h
+	@mkdir -p $(CTEST)
+	$(CC) -O2 -Wall -Wextra -std=gnu11 -Iinclude -o $@ $< $(CLINK) -lpthread
 
 $(BLD)/%.o: $(SRC)/%.c $(wildcard $(SRC)/*.h) $(wildcard include/*/*.h)
 	@mkdir -p $(BLD)

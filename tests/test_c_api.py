@@ -77,3 +77,15 @@ def test_chunk_api_reference_tests_host_route(tmp_path, threads):
         rc, out = _run([_bin("test_chunk_api"), DATA, str(tmp_path), mode],
                        env={"CIOA_CPU_CRC_MAX": str(1 << 62), "CIOA_HOST_CRC_THREADS": threads})
         assert rc == 0 and "0 failed" in out, out
+
+
+@pytest.mark.gpu
+def test_multi_device_host_batches_from_c(cuda, tmp_path):
+    """tests/c/test_multi.c: cio_crc32_batch_host_multi / _fd_multi /
+    cio_crc32_split_host_multi over 1-4 device entries (each with its own host
+    thread, pipeline and stream) and 6 concurrent callers sharing the
+    per-device pipeline pool, every CRC against a bit-serial CRC-32 written in
+    the test."""
+    rc, out = _run([_bin("test_multi"), str(tmp_path)], timeout=300)
+    print(out)
+    assert rc == 0 and "0 failed" in out, out

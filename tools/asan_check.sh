@@ -41,11 +41,11 @@ build)
             $HSAN -c -o $OBJ/$f.o chunkio_amd/csrc/$f.hip
     done
     $HIPCC -shared -fPIC --offload-arch=gfx950 -o $LIBD/libchunkio_amd.so $OBJ/*.o -lpthread
-    for t in test_chunk_api test_crc32_dropin; do
+    for t in test_chunk_api test_crc32_dropin test_multi; do
         $CL -O1 -g -Wall -std=gnu11 $SAN -Iinclude -o $BIN/$t tests/c/$t.c \
-            -L$LIBD -lchunkio_amd -Wl,-rpath,'$ORIGIN/../../../../chunkio_amd/lib/asan'
+            -L$LIBD -lchunkio_amd -Wl,-rpath,'$ORIGIN/../../../../chunkio_amd/lib/asan' -lpthread
     done
-    echo "built $LIBD/libchunkio_amd.so, $BIN/{test_chunk_api,test_crc32_dropin}"
+    echo "built $LIBD/libchunkio_amd.so, $BIN/{test_chunk_api,test_crc32_dropin,test_multi}"
     ;;
 host|gpu)
     DATA=tests/golden/400kb.txt
@@ -64,11 +64,15 @@ host|gpu)
     else
         # Memory errors and UB only: leak checking stays in the host mode (the
         # ROCm runtime's init-time allocations are not freed at exit, and the
-        # library's per-device pipelines are process-lifetime pools).
-        export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1
+        # library's per-device pipelines are process-lifetime pools).  No
+        # quarantine: ROCm's ASan runtime tracks HSA pool allocations, and one
+        # still quarantined when libamdhip64's destructors unload the runtime
+        # trips its "device runtime unloaded" CHECK at exit (seen in r04ao).
+        export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:quarantine_size_mb=0
         for m in immediate deferred; do
             CIOA_CPU_CRC_MAX=0 timeout -k 10 300 $BIN/test_chunk_api $DATA "$W" $m
         done
+        timeout -k 10 300 $BIN/test_multi "$W"
     fi
     echo "asan $MODE: clean"
     ;;
@@ -91,8 +95,10 @@ tsan|tsan-gpu)
                 -Xarch_host -fsanitize=thread -c -o $T/$f.o chunkio_amd/csrc/$f.hip
         done
         $HIPCC -shared -fPIC --offload-arch=gfx950 -o $TL/libchunkio_amd.so $T/*.o -lpthread
-        $CL -O1 -g -std=gnu11 -fsanitize=thread -Iinclude -o $TB/test_chunk_api tests/c/test_chunk_api.c \
-            -L$TL -lchunkio_amd -Wl,-rpath,'$ORIGIN/../../../../chunkio_amd/lib/tsan'
+        for t in test_chunk_api test_multi; do
+            $CL -O1 -g -std=gnu11 -fsanitize=thread -Iinclude -o $TB/$t tests/c/$t.c \
+                -L$TL -lchunkio_amd -Wl,-rpath,'$ORIGIN/../../../../chunkio_amd/lib/tsan' -lpthread
+        done
     fi
     W=$(mktemp -d /tmp/cioa-tsan-XXXXXX)
     trap 'rm -rf "$W"' EXIT
@@ -106,6 +112,10 @@ tsan|tsan-gpu)
                 timeout -k 10 300 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m
         fi
     done
+    if [ "$MODE" = tsan-gpu ]; then
+        TSAN_OPTIONS=halt_on_error=1:suppressions=$PWD/tools/tsan_rocm.supp \
+            timeout -k 10 300 $TB/test_multi "$W"
+    fi
     echo "$MODE: clean"
     ;;
 *)
