@@ -293,6 +293,50 @@ def test_issue_ahead_uniform_aligned_batches(cuda, monkeypatch, grid, l64):
         np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds), want, err_msg=f"one-slot {n}x{ln}")
 
 
+@pytest.mark.parametrize("grid", [None, "4x", 5])
+def test_random_batches_property(cuda, monkeypatch, grid):
+    """Randomised batches (fixed seeds, so a failure reproduces) through every
+    plan path the geometry selects -- uniform aligned (issue-ahead), uniform
+    misaligned, <= 4 KiB (small kernel), log-uniform mixed with empty and
+    tiny chunks, one chunk over many waves -- with and without seeds, on the
+    default grid, the 4-workgroups-per-CU grid and a 5-workgroup grid, in both
+    lane layouts; every CRC against the oracle."""
+    import torch
+    if grid == "4x":
+        monkeypatch.setenv("CIO_GPU_GRID", str(4 * torch.cuda.get_device_properties(cuda).multi_processor_count))
+    elif grid is not None:
+        monkeypatch.setenv("CIO_GPU_GRID", str(grid))
+    rng = np.random.default_rng(0x5EED + (0 if grid is None else 7 if grid == "4x" else grid))
+    cap = 48 << 20
+    for k in range(12):
+        kind = k % 5
+        if kind == 0:                                   # uniform, whole 4 KiB steps, 16-aligned
+            ln = 4096 * int(rng.integers(1, 200))
+            lens = np.full(int(rng.integers(1, max(2, min(600, cap // ln)))), ln, np.uint64)
+        elif kind == 1:                                 # uniform, any length
+            ln = int(rng.integers(1, 300_000))
+            lens = np.full(int(rng.integers(1, max(2, min(400, cap // ln)))), ln, np.uint64)
+        elif kind == 2:                                 # small-chunk kernel
+            lens = rng.integers(0, 4097, int(rng.integers(1, 20_000))).astype(np.uint64)
+        elif kind == 3:                                 # log-uniform mixed, 0 B .. 8 MiB
+            lens = np.floor(np.exp(rng.uniform(0, np.log(8 << 20), int(rng.integers(1, 300))))).astype(np.uint64)
+            lens[rng.random(len(lens)) < 0.1] = 0
+            lens = lens[np.cumsum(lens) <= cap] if lens.sum() > cap else lens
+        else:                                           # one chunk over many waves, tiny ones around it
+            lens = np.concatenate([rng.integers(0, 64, 5), [int(rng.integers(8 << 20, 40 << 20))],
+                                   rng.integers(0, 64, 5)]).astype(np.uint64)
+        if len(lens) == 0:
+            lens = np.asarray([1], np.uint64)
+        buf, offs = wl.host_batch(0xF00D + 31 * k, lens, align=16)
+        if kind != 0:
+            offs = offs + rng.integers(0, 16, len(offs)).astype(np.uint64)
+            buf = np.concatenate([buf, np.zeros(32, np.uint8)])
+        seeds = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32) if k % 2 else None
+        np.testing.assert_array_equal(gpu_crc(cuda, buf, offs, lens, seeds=seeds),
+                                      po.crc_batch(buf, offs, lens, seeds=seeds),
+                                      err_msg=f"batch {k} kind {kind} n {len(lens)} grid {grid}")
+
+
 def test_one_huge_chunk_spans_all_waves(cuda):
     n = 48 * 1024 * 1024 + 12345
     data = wl.gen_chunk(0xBEEF, 0, n)
