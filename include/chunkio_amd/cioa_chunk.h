@@ -30,16 +30,18 @@
  *
  * Where the CRC runs:
  *   - verify on open/up/scan (cio_file_format_check, cio_file.c:266-290): the
- *     batched GPU verify (cio_file_verify_batch_multi); cioa_scan_stream
+ *     batched verify (cio_file_verify_batch_multi, routed by crc_route.c to
+ *     the GPU or, for small batches, the host crc_update); cioa_scan_stream
  *     verifies every chunk it maps in ONE batch;
  *   - the per-write update (update_checksum, cio_file.c:97-113): crc_update
  *     on the caller's buffer, as the reference does -- unless the context
  *     has CIOA_DEFERRED_CRC, where writes only copy and the CRC of every
- *     byte not yet covered is computed at sync time on the GPU, for many
- *     chunks at once with cioa_chunk_sync_batch (cio_file_sync_batch_multi);
+ *     byte not yet covered is computed at sync time (routed the same way),
+ *     for many chunks at once with cioa_chunk_sync_batch
+ *     (cio_file_sync_batch_multi);
  *   - full recomputes (write_at, metadata rewrite: cio_file.c:103-108,
- *     136-140): one GPU batch (immediate mode) or folded into the next sync
- *     (deferred mode).
+ *     136-140): one routed batch (immediate mode) or folded into the next
+ *     sync (deferred mode).
  * Either way the files are byte-identical to the reference's after a sync.
  *
  * Not thread-safe per context, like the reference: one context per thread.
