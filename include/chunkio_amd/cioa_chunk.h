@@ -70,7 +70,7 @@ extern "C" {
 #define CIO_DELETE_IRRECOVERABLE 16
 #define CIO_TRIM_FILES           32
 #endif
-#define CIOA_DEFERRED_CRC        128   /* appends only copy; CRC at sync, on the GPU */
+#define CIOA_DEFERRED_CRC        128   /* appends only copy; CRC at sync, in routed batches */
 
 #ifndef CIO_OK
 #define CIO_OK       0
