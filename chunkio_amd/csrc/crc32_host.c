@@ -206,6 +206,16 @@ uint64_t cioa_crc_update_host(uint64_t crc, const void *data, size_t len)
     uint32_t c = (uint32_t) crc;
 
     pthread_once(&s16_once, build_s16);
+    /* crc_t is 8 bytes and deps/crc32 does not mask on entry: when its first
+     * byte goes through the byte loop (misaligned start, crc32.c:343-348, or
+     * fewer than 8 bytes, :384-386) the shift runs on the 64-bit state, so
+     * bits 32..39 land in bits 24..31; an 8-aligned word step (:366) reads
+     * only the low 32 bits.  Match that, then continue on 32 bits. */
+    if ((crc >> 32) && len && (((uintptr_t) p & 7u) || len < 8)) {
+        c = s16[0][(crc ^ *p) & 0xffu] ^ (uint32_t) (crc >> 8);
+        p++;
+        len--;
+    }
 #if defined(__x86_64__)
     if (len >= 64) {
         pthread_once(&clmul_once, build_clmul);

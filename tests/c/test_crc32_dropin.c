@@ -114,6 +114,50 @@ int main(int argc, char **argv)
         CHECK(cio_crc32_finalize(tmp) == 0x777A8F30u);
     }
     free(buf);
+
+    /* crc_t states with bits 32..63 set (crc32.c does not mask on entry):
+     * the first byte-wise step -- misaligned start (:343-348) or fewer than
+     * 8 bytes (:384-386) -- shifts the 64-bit state, an 8-aligned word step
+     * (:366) reads its low 32 bits.  Checked against a bitwise restatement. */
+    {
+        static const uint64_t wide[] = {0x1FFFFFFFFull, 0xFFFFFFFF12345678ull, 0xABCD00000000ABCDull,
+                                        0xFFFFFFFFFFFFFFFFull, 0x0000000100000000ull};
+        static const size_t lens[] = {0, 1, 2, 3, 7, 8, 9, 15, 16, 17, 63, 64, 65, 1023, 1024, 4093, 409600};
+        unsigned char *al = aligned_alloc(64, n400 + 64);
+        memcpy(al + 8, d400, n400);
+        for (size_t s = 0; s < sizeof(wide) / sizeof(wide[0]); s++) {
+            for (int mis = 0; mis < 8; mis++) {
+                for (size_t l = 0; l < sizeof(lens) / sizeof(lens[0]); l++) {
+                    const unsigned char *p = al + 8 + mis;
+                    size_t len = lens[l];
+                    uint64_t want = wide[s];
+                    size_t i = 0;
+                    if (len && (mis || len < 8)) {
+                        want ^= p[0];
+                        for (int b = 0; b < 8; b++) {
+                            want = (want >> 1) ^ (0xEDB88320u & (0u - (unsigned) (want & 1u)));
+                        }
+                        i = 1;
+                    }
+                    want &= 0xffffffffu;
+                    for (; i < len; i++) {
+                        want ^= p[i];
+                        for (int b = 0; b < 8; b++) {
+                            want = (want >> 1) ^ (0xEDB88320u & (0u - (unsigned) (want & 1u)));
+                        }
+                    }
+                    crc_t got = cio_crc32_update((crc_t) wide[s], p, len);
+                    if ((uint64_t) got != want) {
+                        fprintf(stderr, "wide seed %#llx mis %d len %zu: %#llx != %#llx\n",
+                                (unsigned long long) wide[s], mis, len, (unsigned long long) got,
+                                (unsigned long long) want);
+                        failures++;
+                    }
+                }
+            }
+        }
+        free(al);
+    }
     free(d400);
     if (failures) {
         fprintf(stderr, "%d check(s) failed\n", failures);

@@ -80,6 +80,81 @@ print("ok")
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
 
 
+WIDE_SEEDS_CODE = """
+import sys; sys.path.insert(0, {root!r})
+import numpy as np, chunkio_amd as c
+from oracle import pyoracle as po
+rng = np.random.default_rng(5)
+raw = rng.integers(0, 256, 409600 + 64, dtype=np.uint8)
+a0 = (-raw.ctypes.data) % 8                       # raw[a0:] is 8-byte aligned
+seeds = [0x1FFFFFFFF, 0xFFFFFFFF12345678, 0xABCD00000000ABCD, 0xFFFFFFFFFFFFFFFF,
+         0x0000000100000000, 0xFFFFFFFF, 0xBE26ED00, 0]
+seeds += [int(s) for s in rng.integers(0, 2 ** 63, 4, dtype=np.int64) * 2 + 1]
+lens = list(range(0, 18)) + [63, 64, 65, 1023, 1024, 4093, 409600]
+ref = po.ref()
+diff = n = 0
+for s in seeds:
+    for mis in range(8):
+        for L in lens:
+            ch = raw[a0 + mis:a0 + mis + L]
+            assert ch.ctypes.data % 8 == mis or L == 0
+            got, want = c.crc_update(s, ch), po.crc_update(s, ch)
+            if ref is not None:
+                r = po.crc_update_ref(s, ch)
+                assert want == r, ("oracle vs _ref", hex(s), mis, L, hex(want), hex(r))
+            diff += got != want
+            n += 1
+assert diff == 0, (diff, n)
+print("ok", n, ref is not None)
+"""
+
+
+@pytest.mark.parametrize("mode", ["table", "clmul", "auto"])
+def test_crc_update_wide_crc_t_states(mode):
+    """crc_t is 8 bytes and deps/crc32 does not mask its input: a state with
+    bits 32..63 set folds bits 32..39 into the first byte-wise step
+    (crc32.c:343-348 / :384-386) and drops them on an 8-aligned word step
+    (:366).  The drop-in crc_update (every host path), the oracle and the
+    reference compiled unmodified (oracle/_ref) must agree on every such
+    state, at misalignment 0..7 and lengths around every path switch."""
+    import subprocess
+    import sys
+    code = WIDE_SEEDS_CODE.format(root=ROOT)
+    env = dict(os.environ, CIOA_HOST_CRC=mode)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stderr[-3000:]
+
+
+def test_wide_state_rule_restated_in_python():
+    """The first-step rule, restated without any table library: one bitwise
+    byte step on the full 64-bit state, then the ordinary 32-bit CRC."""
+    def bitwise(c, data):
+        for b in data:
+            c ^= b
+            for _ in range(8):
+                c = (c >> 1) ^ (0xEDB88320 if c & 1 else 0)
+        return c
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.crc_update
+    f.restype = ctypes.c_uint64
+    f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+    buf = (ctypes.c_uint8 * 64)(*range(1, 65))
+    base = ctypes.addressof(buf)
+    seed = 0xABCD005A0000ABCD     # bits 32..39 = 0x5A
+    for start in range(16):
+        p = base + start
+        for L in (1, 5, 7, 8, 9, 40):
+            data = bytes(buf[start:start + L])
+            if (p % 8) or L < 8:
+                t = seed ^ data[0]
+                for _ in range(8):
+                    t = (t >> 1) ^ (0xEDB88320 if t & 1 else 0)
+                want = bitwise(t & 0xFFFFFFFF, data[1:])
+            else:
+                want = bitwise(seed & 0xFFFFFFFF, data)
+            assert f(seed, p, L) == want, (start, L)
+
+
 def test_crc_update_kats(data400):
     assert chunkio_amd.crc32(b"123456789") == 0xCBF43926
     assert chunkio_amd.crc32(b"\0\0") == 0x41D912FF
