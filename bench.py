@@ -120,7 +120,9 @@ def dist_setup(args):
     # than ranks (ranks share devices round-robin, gloo for the barrier and
     # the max-over-ranks).  Never set by the driver's scaling runs.
     rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1"
-    if rehearse:
+    # CIO_BENCH_SHARE_DEVICES=1 (test hook): the same device sharing without
+    # the rehearsal's exemption, so the topology check must fail the line.
+    if rehearse or os.environ.get("CIO_BENCH_SHARE_DEVICES") == "1":
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if args.gpus != world:
@@ -152,6 +154,49 @@ def gather_over_ranks(x, dist, device):
     out = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [float(v.item()) for v in out]
+
+
+def local_topology(device):
+    """Which physical GPU this rank drives: HIP device index, PCI bus ID
+    (cio_gpu_pci_bus_id), NUMA node of its PCIe link, UUID, host."""
+    import ctypes
+    import socket
+    import torch
+    import chunkio_amd as cio
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    buf = ctypes.create_string_buffer(64)
+    bus = buf.value.decode() if cio.lib().cio_gpu_pci_bus_id(idx, buf, 64) == 0 else None
+    try:
+        uuid = str(torch.cuda.get_device_properties(idx).uuid)
+    except (AttributeError, RuntimeError):
+        uuid = None
+    return {"device_index": int(idx), "pci_bus_id": bus, "numa_node": int(cio.lib().cio_gpu_numa_node(idx)),
+            "uuid": uuid, "host": socket.gethostname(), "pid": os.getpid()}
+
+
+def gather_topology(local, dist, rehearse):
+    """Every rank's local_topology() in rank order (gloo all_gather_object).
+    Outside a rehearsal (CIO_BENCH_REHEARSE=1: ranks share the devices of a
+    smaller box on purpose) two ranks on one (host, PCI bus ID) are a broken
+    process layout: a scaling line from it would count one GPU's work N
+    times, so this raises SystemExit on every rank (the launcher then fails
+    the job with a non-zero status)."""
+    if dist is None:
+        topo = [local]
+    else:
+        topo = [None] * dist.get_world_size()
+        dist.all_gather_object(topo, local)
+    keys = [(t.get("host"), t.get("pci_bus_id")) for t in topo]
+    dup = sorted({k for k in keys if keys.count(k) > 1})
+    out = {"ranks": len(topo), "distinct_gpus": len(set(keys)), "rehearsal": bool(rehearse),
+           "device_index": [t.get("device_index") for t in topo],
+           "pci_bus_id": [t.get("pci_bus_id") for t in topo],
+           "numa_node": [t.get("numa_node") for t in topo],
+           "host": sorted({t.get("host") for t in topo})}
+    if dup and not rehearse:
+        raise SystemExit(f"bench.py: ranks share a GPU (host, PCI bus ID) {dup}: "
+                         f"{[(i, k) for i, k in enumerate(keys)]}; refusing to report a {len(topo)}-GPU line")
+    return out
 
 
 def job_digest_matches(local, n_total, want_sha256, dist):
@@ -252,8 +297,21 @@ def cpu_info():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(host_buf, offs, lens, gpu_out):
-    """Reference crc_update (oracle/_ref, 1 thread) over the same batch."""
+def cpu_share(world=1):
+    """Host threads per GPU for the multi-thread CPU figures: the box's CPU
+    share per GPU (16 on the MI355X pool, OMP_NUM_THREADS there), at most this
+    process's affinity divided over the N ranks of the node."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    per_gpu = int(os.environ.get("OMP_NUM_THREADS") or 16)
+    return max(1, min(per_gpu, 16, aff // max(1, world)))
+
+
+def cpu_baseline(host_buf, offs, lens, gpu_out, world=1, reps=64, perf=True):
+    """Reference crc_update (oracle/_ref, 1 thread) over the same batch (at
+    N > 1: rank 0's shard, the same per-GPU batch size)."""
     import ctypes
     from oracle import pyoracle as po
     lib = po.ref()
@@ -265,20 +323,20 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
     offs_c = np.ascontiguousarray(offs, dtype=np.uint64)
     lens_c = np.ascontiguousarray(lens, dtype=np.uint64)
     u64p = ctypes.POINTER(ctypes.c_uint64)
-    reps = 64            # ~10 s of single-thread CPU work at ~2.6 GB/s (the bounded sample)
+    # reps = 64: ~10 s of single-thread CPU work at ~2.6 GB/s (the bounded sample)
     secs = getattr(lib, prefix + "crc_batch_time")(
         host_buf.ctypes.data, offs_c.ctypes.data_as(u64p), lens_c.ctypes.data_as(u64p), n, reps,
         out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     nbytes = float(lens_c.sum()) * reps
     res = {"value": round(nbytes / secs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
-           "sample": f"{n} chunks x {int(lens_c[0]) if n else 0} B (the full cfg2 batch) x {reps} "
+           "sample": f"{n} chunks x {int(lens_c[0]) if n else 0} B (the full per-GPU cfg2 batch) x {reps} "
                      f"passes, crc_update(init, chunk) per chunk, deps/crc32/crc32.c "
                      f"{'compiled from the reference' if kind == 'reference' else 'oracle port'}, -O3",
            "bit_exact_vs_gpu": bool(np.array_equal(out, gpu_out)), **cpu_info()}
     # the same batch over the box's CPU share (16 threads per
     # GPU there), informational; `value`/`cores` above stay the 1-thread
     # reference (chunkio itself is single-threaded).
-    nt = min(16, os.cpu_count() or 1)
+    nt = cpu_share(world)
     f_mt = getattr(lib, prefix + "crc_batch_time_mt", None)
     if f_mt is not None:
         f_mt.restype = ctypes.c_double
@@ -290,7 +348,9 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
                        mreps, nt, out_mt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
         res["multi_thread"] = {"value": round(float(lens_c.sum()) * mreps / secs_mt / 1e9, 3), "unit": "GB/s",
                                "threads": nt, "bit_exact_vs_gpu": bool(np.array_equal(out_mt, gpu_out)),
-                               "sample": f"same batch x {mreps} passes, chunk i on thread i % {nt}"}
+                               "sample": f"same batch x {mreps} passes, chunk i on thread i % {nt}",
+                               "threads_rule": f"per-GPU CPU share at N={world}: min(16, OMP_NUM_THREADS, "
+                                               f"affinity_cpus // N)"}
     # The library's own host path over the same batch (crc_update with
     # VPCLMULQDQ folding, cio_crc32_batch_cpu), 1 thread and the per-GPU CPU
     # share: what a host-resident batch costs without the GPU.  Not the
@@ -298,7 +358,7 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
     try:
         import chunkio_amd as cio
         lib_host = {}
-        for t in sorted({1, host_cpu_threads()}):
+        for t in sorted({1, cpu_share(world)}):
             cio.crc32_batch_cpu_packed(host_buf, offs_c, lens_c, threads=t)
             hreps = 8 if t == 1 else 32
             t0 = time.perf_counter()
@@ -312,6 +372,8 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
     except Exception as e:  # informational
         res["library_host_path"] = {"error": str(e)}
     # tools/cio -k -p restatement (BASELINE config 1), bounded sample of files.
+    if not perf:
+        return res
     try:
         d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8)
         files, writes = 1000, 5
@@ -330,7 +392,7 @@ def cpu_baseline(host_buf, offs, lens, gpu_out):
     return res
 
 
-def cpu_sample_baseline(dev_buf, offs, lens, gpu_out, max_bytes=1 << 30):
+def cpu_sample_baseline(dev_buf, offs, lens, gpu_out, max_bytes=1 << 30, world=1):
     """SURVEY §8(d) CPU item 2 for the cfg3 / cfg4 batches: the reference's
     crc_update (oracle/_ref) on 1 thread and on the box's per-GPU CPU share,
     over a bounded sample of the same batch (its first chunks, <= 1 GiB,
@@ -359,7 +421,7 @@ def cpu_sample_baseline(dev_buf, offs, lens, gpu_out, max_bytes=1 << 30):
     if f_mt is not None:
         f_mt.restype = ctypes.c_double
         f_mt.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, u32p]
-        nt = host_cpu_threads()
+        nt = cpu_share(world)
         out_mt = np.zeros(k, dtype=np.uint32)
         secs_mt = f_mt(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), k, 2, nt,
                        out_mt.ctypes.data_as(u32p))
@@ -593,14 +655,18 @@ def run_crc(args, rank, world, device, dist):
         res["per_gpu"] = {"achieved_GBps": [round(v, 1) for v in gather_over_ranks(achieved, dist, device)],
                           "kernel_ms_mean": [round(v, 5) for v in gather_over_ranks(kernel_ms, dist, device)],
                           "note": "rank order; each rank's algorithmic bytes / its kernel time"}
-    if rank == 0 and world == 1 and not args.no_cpu and args.config == "cfg2":
+    # The reference CPU path beside the line at every N (rank 0, its own
+    # shard: the same per-GPU batch), 1 thread plus the per-GPU CPU share.
+    if rank == 0 and not args.no_cpu and args.config == "cfg2":
         host = bufs[0].cpu().numpy()
-        res["cpu_baseline"] = cpu_baseline(host, offs, lens, gpu0)
-    if rank == 0 and world == 1 and args.config in ("cfg3", "cfg4") and not getattr(args, "no_cpu_sample", args.no_cpu):
+        res["cpu_baseline"] = cpu_baseline(host, offs, lens, gpu0, world=world)
+    if rank == 0 and args.config in ("cfg3", "cfg4", "cfg4k") and not getattr(args, "no_cpu_sample", args.no_cpu):
         try:
-            res["cpu_baseline"] = cpu_sample_baseline(bufs[0], offs, lens, gpu0)
+            res["cpu_baseline"] = cpu_sample_baseline(bufs[0], offs, lens, gpu0, world=world)
         except Exception as e:  # informational
             res["cpu_baseline"] = {"error": str(e)}
+    if "cpu_baseline" in res and world > 1:
+        res["cpu_baseline"]["shard"] = f"rank 0's shard of the {world}-GPU job (the per-GPU batch)"
     plan.close()
     return res
 
@@ -648,6 +714,9 @@ def run_sha1(args, rank, world, device, dist):
             g = json.load(f)["sha1"]
         check["golden_sha256_match_all_digests"] = hashlib.sha256(got.tobytes()).hexdigest() == \
             g["cfg5_sha256_of_digests"]
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = sha1_cpu_baseline(buf.cpu().numpy(), offs, lens, got, world)
     # The bound: one wave's issue rate on the dependent round chain
     # (tools/probe/sha1_round_probe.hip: 20.35 cycles per 5-VALU round at
     # 2.40 GHz, profiles/r02/sha1/sha1_round_probe.txt) times the longest
@@ -673,7 +742,64 @@ def run_sha1(args, rank, world, device, dist):
                          if load_pmc_traffic("sha1", int(lens.sum())) is not None else None},
             "timing": "K launches of cio_sha1_batch_dev_async (device-resident offsets/lengths) back to back, "
                       "host clock between stream syncs",
-            "check": check}
+            "check": check, **({"cpu_baseline": cpu} if cpu is not None else {})}
+
+
+def sha1_cpu_baseline(host, offs, lens, gpu_digests, world=1):
+    """BASELINE.md config 5's CPU path: OpenSSL SHA-1 (Python's hashlib) over
+    the same batch (rank 0's shard at N > 1), one digest per chunk as
+    src/cio_sha1.c:41-57 computes it, on 1 thread and on the per-GPU CPU
+    share; every digest checked against the GPU's."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    views = [memoryview(host[int(o):int(o) + int(n)]) for o, n in zip(offs, lens)]
+    nbytes = float(np.asarray(lens, dtype=np.float64).sum())
+
+    def digests(idx):
+        return [hashlib.sha1(views[i]).digest() for i in idx]
+
+    want = [bytes(d) for d in gpu_digests]
+    t0 = time.perf_counter()
+    reps = 0
+    while True:                      # >= 2 s of single-thread work (the bounded sample)
+        one = digests(range(len(views)))
+        reps += 1
+        if time.perf_counter() - t0 >= 2.0:
+            break
+    secs = time.perf_counter() - t0
+    res = {"value": round(nbytes * reps / secs / 1e9, 4), "unit": "GB/s", "cores": 1,
+           "kind": "openssl (hashlib.sha1)",
+           "sample": f"{len(views)} chunks x {int(lens[0]) if len(lens) else 0} B (the whole per-GPU cfg5 batch) x "
+                     f"{reps} passes, one SHA-1 per chunk",
+           "bit_exact_vs_gpu": one == want,
+           "note": "the reference's own SHA-1 (<sha1/sha1.h>) is not vendored; OpenSSL via hashlib is the "
+                   "CPU path BASELINE.md names for config 5", **cpu_info()}
+    nt = cpu_share(world)
+    if nt > 1:
+        parts = [list(range(t, len(views), nt)) for t in range(nt)]
+        with ThreadPoolExecutor(nt) as ex:
+            list(ex.map(digests, parts))                                   # warm
+            mreps = 0
+            t0 = time.perf_counter()
+            while True:
+                outs = list(ex.map(digests, parts))
+                mreps += 1
+                if time.perf_counter() - t0 >= 1.0:
+                    break
+            secs = time.perf_counter() - t0
+        mt = [None] * len(views)
+        for t, idx in enumerate(parts):
+            for i, d in zip(idx, outs[t]):
+                mt[i] = d
+        res["multi_thread"] = {"value": round(nbytes * mreps / secs / 1e9, 3), "unit": "GB/s", "threads": nt,
+                               "bit_exact_vs_gpu": mt == want,
+                               "sample": f"same batch x {mreps} passes, chunk i on thread i % {nt} "
+                                         "(hashlib releases the GIL while hashing)",
+                               "threads_rule": f"per-GPU CPU share at N={world}: min(16, OMP_NUM_THREADS, "
+                                               f"affinity_cpus // N)"}
+    if world > 1:
+        res["shard"] = f"rank 0's shard of the {world}-GPU job (the per-GPU batch)"
+    return res
 
 
 class E2eDiag:
@@ -1260,7 +1386,7 @@ def spawn_ranks(args):
     children start from a clean process."""
     import subprocess
     visible, _ = visible_gpus()
-    rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1"
+    rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1" or os.environ.get("CIO_BENCH_SHARE_DEVICES") == "1"
     if visible < args.gpus and not rehearse:
         # A sysfs layout this count does not know could under-count: ask the
         # runtime in a child process (this one stays clean for the ranks).
@@ -1343,7 +1469,7 @@ def other_configs(args, rank, world, device, dist, only=None):
         torch.cuda.empty_cache()
         a = copy.copy(args)
         a.config, a.steps, a.warmup = cfg, steps, warm
-        a.no_cpu = cfg != "verify" or args.no_cpu
+        a.no_cpu = cfg not in ("verify", "sha1") or args.no_cpu
         a.no_cpu_sample = args.no_cpu
         t1 = time.perf_counter()
         if cfg == "sha1":
@@ -1378,6 +1504,9 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
     rank, world, device, dist = dist_setup(args)
+    # Before any work: which GPU each rank drives; N ranks on fewer GPUs
+    # fail the line here (outside a rehearsal).
+    topology = gather_topology(local_topology(device), dist, os.environ.get("CIO_BENCH_REHEARSE") == "1")
     if args.config == "sha1":
         res = run_sha1(args, rank, world, device, dist)
     elif args.config == "e2e":
@@ -1402,6 +1531,10 @@ def main():
                                     "order": "run order: e2e, verify, perf (host-memory legs, before any "
                                              "multi-GB HBM free), then other_chunk_sizes, cfg3, sha1"}
             res["diagnostic_batches"] = diagnostic_batches(device)
+    res["topology"] = topology
+    if world > 1:
+        res.setdefault("per_gpu", {}).update(
+            {k: topology[k] for k in ("device_index", "pci_bus_id", "numa_node")})
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

@@ -1183,6 +1183,15 @@ extern "C" int cio_gpu_numa_node(int dev)
     return node;
 }
 
+extern "C" int cio_gpu_pci_bus_id(int dev, char *buf, int len)
+{
+    if (!buf || len < 13) {
+        return cioa::fail("cio_gpu_pci_bus_id: buffer shorter than 13 bytes");
+    }
+    HIP_TRY(hipDeviceGetPCIBusId(buf, len, dev), "hipDeviceGetPCIBusId");
+    return CIO_OK;
+}
+
 extern "C" int cio_gpu_device_count(void)
 {
     int n = 0;

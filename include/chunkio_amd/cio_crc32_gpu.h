@@ -71,6 +71,10 @@ int cio_gpu_get_device(void);            /* -1 on error */
  * the chunk buffers does best to allocate them there too. */
 int cio_gpu_numa_node(int dev);
 
+/* PCI address of device `dev` ("dddd:bb:dd.f", NUL-terminated, len >= 13):
+ * lets one process per GPU show which physical device it drives. */
+int cio_gpu_pci_bus_id(int dev, char *buf, int len);
+
 /* Human-readable reason for the last CIO_ERROR on this thread ("" if none). */
 const char *cio_gpu_last_error(void);
 

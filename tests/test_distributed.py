@@ -350,3 +350,77 @@ def test_bench_job_digest_gathers_shards(world):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert ok is True and nok is False and rok is True
+
+
+def _topology_worker(rank, world, port, rehearse, same_bus, q):
+    import os
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        local = {"device_index": 0 if same_bus else rank, "numa_node": rank,
+                 "pci_bus_id": "0000:05:00.0" if same_bus else f"0000:{5 + rank:02x}:00.0",
+                 "host": "box", "pid": 100 + rank}
+        try:
+            out = bench.gather_topology(local, dist, rehearse)
+            q.put((rank, "ok", out))
+        except SystemExit as e:
+            q.put((rank, "exit", str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same_bus,rehearse,want", [(False, False, "ok"), (True, True, "ok"),
+                                                     (True, False, "exit")])
+def test_bench_topology_gather_gloo_world2(same_bus, rehearse, want):
+    """bench.py records each rank's device index, PCI bus ID and NUMA node
+    (gloo all_gather_object), and two ranks on one GPU fail the line on every
+    rank unless CIO_BENCH_REHEARSE asked for exactly that."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_topology_worker, args=(r, 2, port, rehearse, same_bus, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert [g[1] for g in got] == [want, want]
+    if want == "ok":
+        topo = got[0][2]
+        assert topo == got[1][2]
+        assert topo["numa_node"] == [0, 1] and topo["ranks"] == 2
+        assert topo["distinct_gpus"] == (1 if same_bus else 2)
+        assert topo["pci_bus_id"] == (["0000:05:00.0"] * 2 if same_bus else ["0000:05:00.0", "0000:06:00.0"])
+    else:
+        assert "share a GPU" in got[0][2]
+
+
+def test_bench_cpu_baselines_at_n2():
+    """The CPU legs bench.py puts beside every line, as rank 0 runs them at
+    N = 2: the reference crc32.c (1 thread + the per-GPU share) over a CRC
+    batch, and OpenSSL SHA-1 over a SHA-1 batch, each bit-exact against the
+    expected outputs (the oracle / hashlib stand in for the GPU's here)."""
+    import hashlib
+    import bench
+    from oracle import pyoracle as po
+    rng = np.random.default_rng(4)
+    lens = np.full(64, 4096, dtype=np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = po.crc_batch(host, offs, lens)
+    r = bench.cpu_baseline(host, offs, lens, want, world=2, reps=4, perf=False)
+    assert r["cores"] == 1 and r["kind"] in ("reference", "port") and r["bit_exact_vs_gpu"]
+    assert r["multi_thread"]["threads"] == bench.cpu_share(2) or "multi_thread" not in r
+    assert r["value"] > 0
+    dig = np.frombuffer(b"".join(hashlib.sha1(host[int(o):int(o + n)]).digest() for o, n in zip(offs, lens)),
+                        np.uint8).reshape(-1, 20)
+    s = bench.sha1_cpu_baseline(host, offs, lens, dig, world=2)
+    assert s["cores"] == 1 and s["bit_exact_vs_gpu"] and s["value"] > 0 and s["shard"].startswith("rank 0")
+    if bench.cpu_share(2) > 1:
+        assert s["multi_thread"]["bit_exact_vs_gpu"] and s["multi_thread"]["threads"] == bench.cpu_share(2)
+    bad = dig.copy()
+    bad[3, 0] ^= 1
+    assert not bench.sha1_cpu_baseline(host, offs, lens, bad, world=2)["bit_exact_vs_gpu"]
