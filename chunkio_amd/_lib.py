@@ -23,7 +23,7 @@ EXPORTS = (
     "cio_crc32_plan_exec_events", "cio_crc32_plan_bytes", "cio_crc32_plan_kernel", "cio_crc32_plan_workgroups", "cio_crc32_ring_create", "cio_crc32_ring_exec",
     "cio_crc32_ring_join", "cio_crc32_ring_destroy", "cio_crc32_batch_dev", "cio_crc32_batch_host",
     "cio_crc32_batch_host_multi", "cio_crc32_split_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device", "cio_gpu_numa_node",
-    "cio_gpu_pci_bus_id",
+    "cio_gpu_pci_bus_id", "cio_gpu_plan_cache_stats",
     "cio_crc32_host_register", "cio_crc32_host_unregister", "cio_gpu_pipe_last_timing",
     "cio_crc32_cpu_max", "cio_crc32_set_cpu_max", "cio_crc32_host_threads", "cio_crc32_set_host_threads",
     "cio_crc32_route_reset",
@@ -90,6 +90,7 @@ def _bind(lib):
         "cio_gpu_get_device": (ctypes.c_int, []),
         "cio_gpu_numa_node": (ctypes.c_int, [ctypes.c_int]),
         "cio_gpu_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+        "cio_gpu_plan_cache_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
         "cio_crc32_host_register": (ctypes.c_int, [V, ctypes.c_size_t]),
         "cio_crc32_host_unregister": (ctypes.c_int, [V]),
         "cio_gpu_pipe_last_timing": (ctypes.c_int, [P(ctypes.c_double), ctypes.c_int]),

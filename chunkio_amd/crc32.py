@@ -329,6 +329,14 @@ def pipe_last_timing():
             "plan_ms": round(v[3], 3), "groups": int(v[4]), "staged_bytes": int(v[5])}
 
 
+def plan_cache_stats():
+    """The host pipelines' plan image caches (cio_gpu_plan_cache_stats),
+    summed over the idle pipelines of every device."""
+    v = (ctypes.c_uint64 * 7)()
+    _lib.check(_lib.lib().cio_gpu_plan_cache_stats(v, 7), "cio_gpu_plan_cache_stats")
+    return dict(zip(("entries", "bytes", "hits", "misses", "stores", "evictions", "pipelines"), map(int, v)))
+
+
 def host_register(arr):
     """Pin a long-lived host buffer (numpy array / mmap view) in place so that
     crc32_batch_host DMAs chunks inside it directly (no staging copy)."""

@@ -13,6 +13,12 @@
 
 /* ---- crc32_gpu.hip ------------------------------------------------------ */
 
+/* Diagnostic (round-3 probe, rejected): CIO_DIAG_RS_DYN compiles
+ * read_stream_dyn_kernel, the read-only stream with a dynamically claimed
+ * tail, selected at run time by CIO_GPU_RS_DYN="pool_permille,U,NC"
+ * (tools/rs_dyn_probe.py; `make ablib VAR=rsdyn DEFS=-DCIO_DIAG_RS_DYN`).
+ * Not in the product library. */
+
 /* Diagnostic: lanes read 16 slice / 4 shift table replicas instead of 32 / 8
  * (the 2-way bank conflicts of a two-workgroups-per-CU layout, priced at
  * today's occupancy).  Correct results, slower kernel. */

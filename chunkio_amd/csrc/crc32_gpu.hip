@@ -748,15 +748,15 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     auto issue = [&](StepRegs &r) {
         // Past the wave's range the last step is re-read (cache-resident) so
         // that every refill is the same 4 loads.  AHEAD refills past the
-        // range (its last one or two) read the 4 KiB slice table instead: a
-        // branch-free select keeps one load sequence on every path, so the
-        // compiler's vmcnt waits stay exact, and the table is L2-resident.
+        // range (its last one, or none when CIO_AHEAD_PEEL peels the last
+        // step) use a dummy source chosen branch-free, so one load sequence
+        // serves every path and the compiler's vmcnt waits stay exact: in a
+        // uniform batch chunk 0's first step at base + ua0 (both preloaded
+        // SGPRs -- the slice-table pointer is a kernel argument the hardware
+        // does not preload, and its scalar load held every wave's first HBM
+        // request), otherwise the L2-resident 4 KiB slice table.
         if (AHEAD) {
             const bool real = nload > 0;
-            // Uniform batches re-read chunk 0's first step instead (base and
-            // ua0 are preloaded SGPRs): the table pointer is a kernel argument
-            // the hardware does not preload, and its scalar load held every
-            // wave's first HBM request.
             const uint8_t *src = real ? lbase + ld.a
                                : UNIFORM ? base + ua0 : reinterpret_cast<const uint8_t *>(g_slice);
             if (L64) {
@@ -1696,6 +1696,7 @@ fill_kernel(uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     }
 }
 
+#if defined(CIO_DIAG_RS_DYN)
 // Diagnostic (CIO_GPU_RS_DYN="pool_permille,U,NC"): the read-only stream with
 // a dynamic tail.  The first S - P steps are split evenly over the waves as
 // in read_stream_kernel; the last P steps form a pool of U-step units, dealt
@@ -1755,6 +1756,7 @@ read_stream_dyn_kernel(const uint8_t *__restrict__ base, uint64_t S, uint64_t Ss
         sink[wave] = x;
     }
 }
+#endif  // CIO_DIAG_RS_DYN
 
 // ---------------------------------------------------------------- host side
 
@@ -2176,6 +2178,27 @@ struct cio_crc32_ring {
     std::vector<hipEvent_t> ready, done;    // per slot: caller's inputs, slot's last batch
     std::vector<bool> pending;              // slot has work the caller has not joined
     unsigned next = 0;
+    int dev = 0;                            // device the plans and streams live on
+};
+
+// Makes `dev` current for one scope and restores the caller's device after:
+// a ring's plans, streams and events belong to the device current at create.
+struct RingDevice {
+    int prev = -1;
+    hipError_t e = hipSuccess;
+    explicit RingDevice(int dev)
+    {
+        if ((e = hipGetDevice(&prev)) == hipSuccess && prev != dev) {
+            e = hipSetDevice(dev);
+        }
+    }
+    ~RingDevice()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) {
+            (void) hipSetDevice(prev);
+        }
+    }
 };
 
 void cio_crc32_ring_destroy(cio_crc32_ring *r)
@@ -2183,6 +2206,7 @@ void cio_crc32_ring_destroy(cio_crc32_ring *r)
     if (!r) {
         return;
     }
+    RingDevice on(r->dev);
     for (hipStream_t st : r->streams) {
         if (st) (void) hipStreamSynchronize(st);
     }
@@ -2204,7 +2228,10 @@ int cio_crc32_ring_create(cio_crc32_ring **out, const uint64_t *offs, const uint
     if (depth < 1 || depth > 8) {
         return fail("cio_crc32_ring_create: depth must be 1..8");
     }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "cio_crc32_ring_create: hipGetDevice");
     cio_crc32_ring *r = new cio_crc32_ring();
+    r->dev = dev;
     r->plans.assign((size_t) depth, nullptr);
     r->streams.assign((size_t) depth, nullptr);
     r->ready.assign((size_t) depth, nullptr);
@@ -2233,7 +2260,9 @@ int cio_crc32_ring_exec(cio_crc32_ring *r, const void *dev_base, const uint32_t 
     if (!r) {
         return fail("cio_crc32_ring_exec: null ring");
     }
-    const size_t i = r->next++ % r->plans.size();
+    RingDevice on(r->dev);
+    HIP_TRY(on.e, "cio_crc32_ring_exec: hipSetDevice");
+    const size_t i = r->next % r->plans.size();
     const hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
     // the batch waits for everything the caller queued before it (its inputs);
     // the slot's stream orders it after the slot's previous batch (scratch reuse)
@@ -2244,6 +2273,7 @@ int cio_crc32_ring_exec(cio_crc32_ring *r, const void *dev_base, const uint32_t 
     }
     HIP_TRY(hipEventRecord(r->done[i], r->streams[i]), "cio_crc32_ring_exec: hipEventRecord");
     r->pending[i] = true;
+    r->next++;      // only a batch that was queued moves the ring on
     return CIO_OK;
 }
 
@@ -2252,6 +2282,8 @@ int cio_crc32_ring_join(cio_crc32_ring *r, void *stream)
     if (!r) {
         return fail("cio_crc32_ring_join: null ring");
     }
+    RingDevice on(r->dev);
+    HIP_TRY(on.e, "cio_crc32_ring_join: hipSetDevice");
     const hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
     for (size_t i = 0; i < r->plans.size(); i++) {
         if (r->pending[i]) {
@@ -2558,6 +2590,7 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
         const int lb = atoi(r);
         work |= (lb == 64 ? 2u : lb == 32 ? 1u : 0u) << 16;
     }
+#if defined(CIO_DIAG_RS_DYN)
     if (const char *r = getenv("CIO_GPU_RS_DYN")) {
         unsigned pm = 0, U = 4, NC = 64;
         if (sscanf(r, "%u,%u,%u", &pm, &U, &NC) >= 1 && pm > 0 && pm <= 1000 && U >= 1 && NC >= 1 &&
@@ -2584,6 +2617,7 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
             return CIO_OK;
         }
     }
+#endif
     if (ev0) {
         HIP_TRY(hipEventRecord(ev0, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
     }

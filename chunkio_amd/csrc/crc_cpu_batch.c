@@ -55,7 +55,27 @@ struct cpu_job {
     int failed;                 /* atomic: a file range could not be read */
 };
 
-static __thread unsigned char *t_readbuf;
+/* pread bounce buffer per thread (file sources), freed when its thread
+ * exits (a caller thread routes fd batches here too, and services spawn and
+ * end such threads). */
+static pthread_key_t g_rb_key;
+static pthread_once_t g_rb_once = PTHREAD_ONCE_INIT;
+
+static void rb_key_make(void)
+{
+    (void) pthread_key_create(&g_rb_key, free);
+}
+
+static unsigned char *thread_readbuf(void)
+{
+    (void) pthread_once(&g_rb_once, rb_key_make);
+    unsigned char *b = pthread_getspecific(g_rb_key);
+    if (!b && (b = malloc(kReadBuf)) != NULL && pthread_setspecific(g_rb_key, b) != 0) {
+        free(b);
+        b = NULL;
+    }
+    return b;
+}
 
 static int run_piece(const struct cpu_job *j, const struct piece *pc, uint32_t *out)
 {
@@ -66,7 +86,8 @@ static int run_piece(const struct cpu_job *j, const struct piece *pc, uint32_t *
         *out = (uint32_t) crc_update(seed, p, (size_t) pc->len);
         return 0;
     }
-    if (!t_readbuf && !(t_readbuf = malloc(kReadBuf))) {
+    unsigned char *t_readbuf = thread_readbuf();
+    if (!t_readbuf) {
         return -1;
     }
     crc_t c = seed;

@@ -25,7 +25,7 @@
  * so the host wins below B* = kGpuFixedUs / (1/r_host - 1/r_gpu), and for
  * every size once r_host >= r_gpu.  With chunkio's one thread (T = 1, the
  * default: the reference is single-threaded and so is Fluent Bit's caller)
- * B* is ~11 MB per device (measured crossovers: between 52 and 105 MB on
+ * B* is ~17 MB per device (measured crossovers: between 52 and 105 MB on
  * the fast box, between 13 and 26 MB on the slow one).  With T >= 2 host threads the host's DRAM rate
  * already beats one PCIe link, so host-resident batches stay on the CPU: the
  * GPU path pays off for host-resident chunks only when the caller cannot
@@ -49,12 +49,16 @@
  * pageable memory): the GPU host batch's least-squares fixed cost and rate
  * (profiles/r04/route_batch_r04d.json: 163.5 us, 54.7 GB/s), and
  * crc_update's rate on one thread and on 16, which differ by box (r04a:
- * 47.6 / 396 GB/s; r04d: 27.4 / 131 GB/s).  The host rates are taken near
- * the slower box, so an ambiguous batch goes to the GPU and leaves the
- * host's cores to the caller. */
+ * 47.6 / 396 GB/s; r04d: 27.4 / 131 GB/s over the whole sweep).  The
+ * one-thread rate is the slower box's where the crossover lies -- 13 to
+ * 52 MB batches run at 36-40 GB/s there (its 27.4 GB/s fit is pulled down
+ * by the 100-400 MB batches) -- so the model's crossover, ~17 MB, falls
+ * between that box's measured 13 MB (host faster) and 26 MB (GPU faster)
+ * and below the faster box's 52-105 MB: an ambiguous batch still goes to
+ * the GPU and leaves the host's cores to the caller. */
 static const double kGpuFixedUs = 163.5;
 static const double kGpuGBps = 54.7;
-static const double kCpuThreadGBps = 30.0;
+static const double kCpuThreadGBps = 36.0;
 static const double kCpuMemGBps = 131.0;
 
 static size_t g_cpu_max;

@@ -377,19 +377,29 @@ struct PipeSlot {
 // recur -- the chunk layer's syncs of equal-sized chunks, a scan of
 // equal-sized files, a benchmark's repeated batch -- and building a group's
 // plan (ChunkDesc / WaveStart / fold factors for 4096 waves, ~0.1 ms) then
-// costs more than copying its ~330 KB image.  The key is the whole geometry
-// (offsets, lengths, chunk ids, wave count), compared in full on a hit.
-struct PlanImage {
-    uint64_t hash = 0;
+// costs more than copying its ~330 KB image.  The key is a 128-bit digest of
+// the whole geometry (offsets, lengths, chunk ids, wave count: two
+// independent 64-bit hashes), not a copy of it, so an entry holds only its
+// image.  Entries are admitted on a geometry's SECOND sighting (a stream of
+// never-repeating batches -- the chunk layer's varying sync batches -- stores
+// nothing) and the cache is capped in bytes per pipeline.
+struct GeoKey {
+    uint64_t a = 0, b = 0;
     uint32_t W = 0;
-    std::vector<uint64_t> offs, lens;
-    std::vector<uint32_t> cid;
+    uint64_t n = 0;
+    bool operator==(const GeoKey &o) const { return a == o.a && b == o.b && W == o.W && n == o.n; }
+};
+
+struct PlanImage {
+    GeoKey key;
     std::vector<uint8_t> image;
     size_t o_desc = 0, o_ws = 0, o_tiny = 0, o_pfac = 0, o_cid = 0, npfac = 0;
     uint64_t S = 0, bytes = 0;
     uint32_t ntiny = 0;
     uint64_t used = 0;               // LRU clock
 };
+
+constexpr int kSeen = 64;            // recent misses remembered for admission
 
 struct HostPipe {
     bool ready = false;
@@ -398,11 +408,17 @@ struct HostPipe {
     uint32_t *state = nullptr;       // running raw CRC per chunk of the call
     size_t state_cap = 0;
     std::vector<PlanImage> plans;    // plan image cache (one pipeline = one caller at a time)
+    size_t plan_bytes = 0;           // sum of the cached images
     uint64_t plan_clock = 0;
+    GeoKey seen[kSeen];              // ring of geometries seen once (admission filter)
+    int seen_next = 0;
+    uint64_t hits = 0, misses = 0, stores = 0, evictions = 0;
 };
 
-// Plan image cache size per pipeline (CIO_GPU_PLAN_CACHE entries, default
-// 32, 0 = off); entries are ~330 KB for a 64 MiB group of 400 KB chunks.
+// Plan image cache limits per pipeline: CIO_GPU_PLAN_CACHE entries (default
+// 32, 0 = off) and CIO_GPU_PLAN_CACHE_MB megabytes (default 16; an image
+// larger than a quarter of it is never cached).  A 64 MiB group of 400 KB
+// chunks is ~330 KB; of 4 KiB chunks ~1.3 MB.
 static size_t plan_cache_entries()
 {
     static const size_t v = [] {
@@ -418,21 +434,47 @@ static size_t plan_cache_entries()
     return v;
 }
 
-static uint64_t geometry_hash(const HostGroup &g, uint32_t W)
+static size_t plan_cache_bytes()
 {
-    uint64_t h = 0xcbf29ce484222325ull ^ W;
+    static const size_t v = [] {
+        long mb = 16;
+        if (const char *r = getenv("CIO_GPU_PLAN_CACHE_MB")) {
+            mb = atol(r);
+            if (mb < 0 || mb > 4096) {
+                mb = 16;
+            }
+        }
+        return (size_t) mb << 20;
+    }();
+    return v;
+}
+
+static GeoKey geometry_key(const HostGroup &g, uint32_t W)
+{
+    // FNV-1a-style and a multiply-xorshift over the same words, different
+    // constants: a false match needs both 64-bit digests to collide.
+    uint64_t h1 = 0xcbf29ce484222325ull ^ W, h2 = 0x9E3779B97F4A7C15ull + W;
     auto mix = [&](uint64_t x) {
-        h ^= x;
-        h *= 0x100000001b3ull;
-        h ^= h >> 29;
+        h1 ^= x;
+        h1 *= 0x100000001b3ull;
+        h1 ^= h1 >> 29;
+        h2 += x * 0xbf58476d1ce4e5b9ull;
+        h2 ^= h2 >> 31;
+        h2 *= 0x94d049bb133111ebull;
     };
-    mix(g.offs.size());
-    for (size_t i = 0; i < g.offs.size(); i++) {
+    const size_t n = g.offs.size();
+    mix(n);
+    for (size_t i = 0; i < n; i++) {
         mix(g.offs[i]);
         mix(g.lens[i]);
         mix(g.cid[i]);
     }
-    return h;
+    GeoKey k;
+    k.a = h1;
+    k.b = h2;
+    k.W = W;
+    k.n = n;
+    return k;
 }
 
 // Pipelines are pooled per device: a call takes an idle one (or builds one,
@@ -574,13 +616,17 @@ hipError_t stage_plan(HostPipe &hp, PipeSlot &s, const HostGroup &g, DeviceState
     const size_t n = g.offs.size();
     plan_init(&view, st, n);
     const size_t ncache = plan_cache_entries();
-    const uint64_t h = ncache ? geometry_hash(g, view.W) : 0;
+    GeoKey key;
     PlanImage *hit = nullptr;
-    for (auto &pi : hp.plans) {
-        if (pi.hash == h && pi.W == view.W && pi.offs == g.offs && pi.lens == g.lens && pi.cid == g.cid) {
-            hit = &pi;
-            break;
+    if (ncache) {
+        key = geometry_key(g, view.W);
+        for (auto &pi : hp.plans) {
+            if (pi.key == key) {
+                hit = &pi;
+                break;
+            }
         }
+        hit ? hp.hits++ : hp.misses++;
     }
     PlanImage built;
     if (!hit) {
@@ -630,18 +676,30 @@ hipError_t stage_plan(HostPipe &hp, PipeSlot &s, const HostGroup &g, DeviceState
     *meta_bytes = total;
     hit->used = ++hp.plan_clock;
     if (hit == &built && ncache) {
-        // keep it: evict the least recently used entry when full
-        built.hash = h;
-        built.W = view.W;
-        built.offs = g.offs;
-        built.lens = g.lens;
-        built.cid = g.cid;
-        if (hp.plans.size() < ncache) {
+        // Admit on the second sighting only, then evict least recently used
+        // entries until both the entry and the byte caps hold.
+        bool seen_before = false;
+        for (const auto &k : hp.seen) {
+            seen_before |= (k == key);
+        }
+        const size_t sz = built.image.size();
+        if (!seen_before) {
+            hp.seen[hp.seen_next] = key;
+            hp.seen_next = (hp.seen_next + 1) % kSeen;
+        } else if (sz <= plan_cache_bytes() / 4) {
+            while (!hp.plans.empty() &&
+                   (hp.plans.size() >= ncache || hp.plan_bytes + sz > plan_cache_bytes())) {
+                auto lru = std::min_element(hp.plans.begin(), hp.plans.end(),
+                                            [](const PlanImage &a, const PlanImage &b) { return a.used < b.used; });
+                hp.plan_bytes -= lru->image.size();
+                std::iter_swap(lru, hp.plans.end() - 1);
+                hp.plans.pop_back();
+                hp.evictions++;
+            }
+            built.key = key;
+            hp.plan_bytes += sz;
             hp.plans.push_back(std::move(built));
-        } else {
-            auto lru = std::min_element(hp.plans.begin(), hp.plans.end(),
-                                        [](const PlanImage &a, const PlanImage &b) { return a.used < b.used; });
-            *lru = std::move(built);
+            hp.stores++;
         }
     }
     return hipSuccess;
@@ -1171,6 +1229,31 @@ extern "C" int cio_gpu_pipe_last_timing(double *out, int n)
     }
     const double v[6] = {pt.total_ms, pt.copy_ms, pt.slot_wait_ms, pt.plan_ms, pt.groups, pt.bytes};
     for (int i = 0; i < n && i < 6; i++) {
+        out[i] = v[i];
+    }
+    return CIO_OK;
+}
+
+extern "C" int cio_gpu_plan_cache_stats(uint64_t *out, int n)
+{
+    if (!out) {
+        return cioa::fail("cio_gpu_plan_cache_stats: null pointer");
+    }
+    uint64_t v[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int d = 0; d < kMaxDev; d++) {
+        DevPipes &dp = g_pipes[d];
+        std::lock_guard<std::mutex> lk(dp.mu);
+        for (const HostPipe *hp : dp.idle) {
+            v[0] += hp->plans.size();
+            v[1] += hp->plan_bytes;
+            v[2] += hp->hits;
+            v[3] += hp->misses;
+            v[4] += hp->stores;
+            v[5] += hp->evictions;
+            v[6] += 1;
+        }
+    }
+    for (int i = 0; i < n && i < 7; i++) {
         out[i] = v[i];
     }
     return CIO_OK;

@@ -215,6 +215,13 @@ int  cio_crc32_host_unregister(const void *p);
  * Fills min(n, 6) values. */
 int  cio_gpu_pipe_last_timing(double *out, int n);
 
+/* The host pipelines' plan image caches, summed over every idle pipeline of
+ * every device: {entries, bytes held, hits, misses, stores, evictions,
+ * pipelines}.  Fills min(n, 7) values.  A geometry is cached on its second
+ * sighting; each pipeline holds at most CIO_GPU_PLAN_CACHE entries (32) and
+ * CIO_GPU_PLAN_CACHE_MB megabytes (16). */
+int  cio_gpu_plan_cache_stats(uint64_t *out, int n);
+
 /* ---- batched CRC-32 on the host CPU ------------------------------------ */
 
 /* The same batch as cio_crc32_batch_host / _fd_multi computed on the host:
@@ -239,7 +246,7 @@ int  cio_crc32_batch_fd_cpu(const int *fds, const uint64_t *foffs, const size_t 
  * batches on the GPU (cio_crc32_batch_host_multi / _fd_multi).  Same results
  * either way.  The default threshold is a cost model with rates measured on
  * the MI355X box (crc_route.c): with the default single host thread it is
- * ~11 MB per device in the call's device list; with two or more host threads
+ * ~17 MB per device in the call's device list; with two or more host threads
  * the host's DRAM rate beats a PCIe link and every host-memory batch stays on
  * the CPU.  CIOA_CPU_CRC_MAX (bytes) or cio_crc32_set_cpu_max() override the
  * threshold, 0 sends everything to the GPU; CIOA_HOST_CRC_THREADS or

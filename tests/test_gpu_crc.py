@@ -497,6 +497,38 @@ def test_ring_batches_overlap_same_results(cuda, depth):
             cio.Crc32Ring(offs, lens, depth=bad)
 
 
+def test_ring_runs_on_its_own_device_and_restores_the_callers(cuda):
+    """A ring belongs to the device current at create: exec / join / close
+    after the caller switched devices (cio_gpu_set_device to another ordinal,
+    ordinal 0 again on a one-GPU box) still run on the ring's device, give
+    the plan's CRCs, and leave the caller's device current."""
+    import torch
+    lib = cio.lib()
+    ndev = cio.device_count()
+    lens = np.full(64, 409600, np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    buf = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(buf, offs, lens, 0x77)
+    want = po.crc_batch(buf.cpu().numpy(), offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=cuda)
+    assert lib.cio_gpu_set_device(0) == 0
+    ring = cio.Crc32Ring(offs, lens, depth=2)
+    other = 1 % ndev
+    try:
+        assert lib.cio_gpu_set_device(other) == 0
+        s = torch.cuda.current_stream(cuda)
+        ring.exec(buf, out, stream=s)
+        assert lib.cio_gpu_get_device() == other
+        ring.join(stream=s)
+        assert lib.cio_gpu_get_device() == other
+        torch.cuda.synchronize(cuda)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    finally:
+        ring.close()
+        assert lib.cio_gpu_get_device() == other
+        lib.cio_gpu_set_device(0)
+
+
 @pytest.mark.parametrize("ndev", [1, 2, 3, 8])
 def test_split_one_buffer_over_devices(cuda, ndev):
     """cio_crc32_split_host_multi: one buffer cut into a piece per (logical)
@@ -646,6 +678,42 @@ def test_host_plan_cache_same_geometry_new_data(cuda):
         for o, ln in ((offs, lens), (offs, lens2), (offs[perm], lens[perm])):
             want = po.crc_batch(host, o, ln, seeds=seeds)
             np.testing.assert_array_equal(cio.crc32_batch_host_packed(host, o, ln, seeds=seeds), want)
+
+
+@pytest.mark.gpu
+def test_host_plan_cache_admission_and_byte_cap(cuda):
+    """The plan image cache stores a geometry on its second sighting only and
+    stays under its byte cap: 40 host batches that never repeat a geometry
+    store nothing and leave the held bytes where they were; one geometry
+    called three times is stored once and hit once; 60 distinct geometries
+    each seen twice keep every pipeline under CIO_GPU_PLAN_CACHE_MB (16)."""
+    rng = np.random.default_rng(77)
+    s0 = cio.plan_cache_stats()
+    for k in range(40):
+        lens = rng.integers(1, 300_000, 64 + k).astype(np.uint64)
+        host, offs = wl.host_batch(0x51 + k, lens, align=16)
+        want = po.crc_batch(host, offs, lens)
+        np.testing.assert_array_equal(cio.crc32_batch_host_packed(host, offs, lens), want)
+    s1 = cio.plan_cache_stats()
+    assert s1["stores"] == s0["stores"] and s1["bytes"] == s0["bytes"], (s0, s1)
+    assert s1["misses"] - s0["misses"] >= 40
+    lens = rng.integers(1, 300_000, 50).astype(np.uint64)
+    host, offs = wl.host_batch(0x99, lens, align=16)
+    want = po.crc_batch(host, offs, lens)
+    for _ in range(3):
+        np.testing.assert_array_equal(cio.crc32_batch_host_packed(host, offs, lens), want)
+    s2 = cio.plan_cache_stats()
+    assert s2["stores"] - s1["stores"] == 1 and s2["hits"] - s1["hits"] >= 1, (s1, s2)
+    # small chunks make large images (~1.3 MB per 64 MiB group of 4 KiB chunks)
+    for k in range(60):
+        lens = np.full(2000 + 37 * k, 4096 - (k % 7), dtype=np.uint64)
+        host, offs = wl.host_batch(0x700 + k, lens, align=16)
+        for _ in range(2):
+            cio.crc32_batch_host_packed(host, offs, lens)
+    s3 = cio.plan_cache_stats()
+    assert s3["stores"] > s2["stores"] and s3["evictions"] > s2["evictions"], (s2, s3)
+    assert s3["bytes"] <= 16 * (1 << 20) * s3["pipelines"], s3
+    assert s3["entries"] <= 32 * s3["pipelines"], s3
 
 
 def test_host_pipeline_reuse_and_growth(cuda):

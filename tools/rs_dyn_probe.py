@@ -9,6 +9,10 @@ read-only stream (read_stream_kernel, the CRC kernel's split) against
 read_stream_dyn_kernel (CIO_GPU_RS_DYN = pool permille, unit steps,
 counters), interleaved, every launch bracketed by its own event pair around
 the kernel alone (the counter reset is outside the pair).  Mean / median us.
+
+The dynamic kernel is not in the product library (round 5): build
+`make ablib VAR=rsdyn DEFS=-DCIO_DIAG_RS_DYN` and run with
+CIO_AMD_LIB=chunkio_amd/lib/ab/rsdyn.so.
 """
 import ctypes
 import os
