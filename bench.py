@@ -241,6 +241,12 @@ def geometry(cfg, rank, world):
     if cfg == "cfg3":
         ids = np.arange(rank, wl.CFG3_N * world, world, dtype=np.uint64)  # weak: 65536 per GPU
         lens = wl.cfg3_lens(wl.CFG3_N * world)[ids.astype(np.int64)]
+        rnd = int(os.environ.get("CIO_BENCH_CFG3_ROUND", "0"))
+        if rnd:
+            # diagnostic (traffic attribution, profiles/r05/cfg3_traffic/): every
+            # length rounded up to a multiple of `rnd` (and offsets aligned to
+            # it in run_crc), same kernel and grid; checks no longer apply
+            lens = (lens + np.uint64(rnd - 1)) // np.uint64(rnd) * np.uint64(rnd)
         desc = {"workload": "cfg3: 65536 mixed chunks per GPU, len=floor(4096*1024^u), "
                             "persistent load-balanced kernel", "chunks_per_gpu": int(len(ids)),
                 "bytes_per_gpu": int(lens.sum())}
@@ -436,7 +442,11 @@ def run_crc(args, rank, world, device, dist):
     from chunkio_amd import workloads as wl
 
     lens, ids, seed, desc, scaling = geometry(args.config, rank, world)
-    offs = wl.packed_offsets(lens, align=16)
+    align = 16
+    if args.config == "cfg3" and os.environ.get("CIO_BENCH_CFG3_ROUND"):
+        align = max(16, int(os.environ["CIO_BENCH_CFG3_ROUND"]))
+        desc["diagnostic_round"] = align
+    offs = wl.packed_offsets(lens, align=align)
     total = wl.batch_bytes(offs, lens)
     nrot = N_ROTATE if total * N_ROTATE < 64e9 else 1
     bufs = []

@@ -65,6 +65,25 @@
 #define CIO_SMALL_EXP 0
 #endif
 
+/* Alignment of a chunk's virtual start for chunks longer than one 4 KiB
+ * step: 16 (shipped through round 4) or 128 (one L2 line).  At 128 every
+ * 1 KiB row of such a chunk is line-aligned, so consecutive rows and steps
+ * never share a line; the head (up to 127 bytes of the neighbour) is zeroed
+ * in registers as the 16-byte head always was.  Chunks of at most one step
+ * keep 16 (they stay on the small-chunk kernel). */
+#ifndef CIO_HEAD_ALIGN
+#define CIO_HEAD_ALIGN 16
+#endif
+
+/* Small-chunk kernel, L64 layout (CIO_GPU_L64=1): the lane's final multiply by
+ * x^(8 * 64 (63 - L)) as 8 nibble-table lookups in the LDS the L64 layout
+ * leaves free (the 32 KiB shift-table region: [nibble position j][nibble]
+ * [lane] words, built per workgroup from the lane's register matrix) instead
+ * of 32 bit-select + fused and-xor instructions. */
+#ifndef CIO_SMALL_NIBFOLD
+#define CIO_SMALL_NIBFOLD 0
+#endif
+
 /* ---- sha1_gpu.hip -------------------------------------------------------- */
 
 /* A/B: blocks handed over per barrier, schedule waves, chunks per workgroup

@@ -329,7 +329,7 @@ __device__ __forceinline__ void table_entries(uint32_t k, uint32_t b, uint32_t &
 constexpr int kE = 1024 / kThreads;            // table entries per thread
 static_assert(kE == 1, "one slice and one shift entry per thread");
 
-template <bool STAMPS = false>
+template <bool STAMPS = false, bool SHIFT = true>
 __device__ __forceinline__ void write_tables(char *lds, uint32_t tid, const uint32_t (&tab_v)[kE],
                                              const uint32_t (&tab_sv)[kE], unsigned long long *ts = nullptr)
 {
@@ -340,11 +340,13 @@ __device__ __forceinline__ void write_tables(char *lds, uint32_t tid, const uint
     for (int i = 0; i < 8; ++i) {
         *reinterpret_cast<uint4 *>(lds + srow + 16u * ((lane + (uint32_t) i) & 7u)) = sv;
     }
-    const uint32_t hrow = kShiftOff + k * 8192u + b * 32u;
-    const uint4 hv = make_uint4(tab_sv[0], tab_sv[0], tab_sv[0], tab_sv[0]);
+    if (SHIFT) {
+        const uint32_t hrow = kShiftOff + k * 8192u + b * 32u;
+        const uint4 hv = make_uint4(tab_sv[0], tab_sv[0], tab_sv[0], tab_sv[0]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        *reinterpret_cast<uint4 *>(lds + hrow + 16u * ((lane + (uint32_t) i) & 1u)) = hv;
+        for (int i = 0; i < 2; ++i) {
+            *reinterpret_cast<uint4 *>(lds + hrow + 16u * ((lane + (uint32_t) i) & 1u)) = hv;
+        }
     }
     if (STAMPS) {
         ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -451,7 +453,7 @@ __device__ __forceinline__ void slow_compute(const char *lds, uint32_t lb_lo, ui
             continue;
         }
         uint32_t w[4] = {r.q[q].x, r.q[q].y, r.q[q].z, r.q[q].w};
-        if (q == 0 && jj == 0 && lane < 2) {
+        if (q == 0 && jj == 0 && 16 * lane < h + 4) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int off = (int) (16 * lane) + 4 * i - (int) h;
@@ -504,7 +506,7 @@ __device__ __forceinline__ void slow_compute64(const char *lds, uint32_t lb_lo, 
             continue;
         }
         uint32_t w[4] = {r.q[k].x, r.q[k].y, r.q[k].z, r.q[k].w};
-        if (jj == 0 && lane == 0 && k < 2) {
+        if (jj == 0 && 64 * lane + 16 * (uint32_t) k < h + 4) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int off = 16 * k + 4 * i - (int) h;
@@ -881,9 +883,14 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
                         if (AHEAD) {
                             r.q[0].x ^= lane == 0 ? seed : 0u;   // h = 0: the seed on content bytes 0..3
                         } else {
-                            // head bytes and seed: granules 0 and 1 of lane 0 (4 L + k)
+                            // head bytes and seed: granules 0 and 1 of lane 0 (4 L + k);
+                            // with 128-byte heads, granules 0..8 (lanes 0..2)
                             r.q[0] = head_fix(r.q[0], 4u * lane, d.h, seed);
                             r.q[1] = head_fix(r.q[1], 4u * lane + 1u, d.h, seed);
+                            if (CIO_HEAD_ALIGN > 16) {
+                                r.q[2] = head_fix(r.q[2], 4u * lane + 2u, d.h, seed);
+                                r.q[3] = head_fix(r.q[3], 4u * lane + 3u, d.h, seed);
+                            }
                         }
                     }
                     uint32_t st = block16(lds, lb_lo, lb_hi, h0, r.q[0]);
@@ -1245,6 +1252,51 @@ struct SmallRegs {
 };
 
 
+// CIO_SMALL_NIBFOLD (cio_diag.h): M_L s for the lane's matrix M_L as 8 nibble
+// lookups.  Table layout in the shift-table region: word (j, nib, lane) at
+// kShiftOff + j * 4096 + nib * 256 + lane * 4 = M_L (nib << 4 j), so the 32
+// lanes of a half-wave read 32 different banks whatever the nibbles.
+// Wave w of the workgroup writes nibble position j = w / 2, nibbles
+// 8 (w & 1) .. + 8, from columns 4 j .. 4 j + 3 of its lanes' matrices.
+template <int J>
+__device__ __forceinline__ void nib_rows(char *lds, uint32_t lane4, const uint32_t (&col)[32], uint32_t half)
+{
+    const uint32_t c0 = col[4 * J], c1 = col[4 * J + 1], c2 = col[4 * J + 2];
+    const uint32_t c3 = col[4 * J + 3] & (0u - half);
+    char *t = lds + kShiftOff + (uint32_t) J * 4096u + half * 2048u + lane4;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t v = ((k & 1) ? c0 : 0u) ^ ((k & 2) ? c1 : 0u) ^ ((k & 4) ? c2 : 0u) ^ c3;
+        *reinterpret_cast<uint32_t *>(t + (uint32_t) k * 256u) = v;
+    }
+}
+
+__device__ __forceinline__ void write_nib_tables(char *lds, uint32_t tid, const uint32_t (&col)[32])
+{
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane4 = (tid & 63u) << 2, half = w & 1u;
+    switch (w >> 1) {
+    case 0: nib_rows<0>(lds, lane4, col, half); break;
+    case 1: nib_rows<1>(lds, lane4, col, half); break;
+    case 2: nib_rows<2>(lds, lane4, col, half); break;
+    case 3: nib_rows<3>(lds, lane4, col, half); break;
+    case 4: nib_rows<4>(lds, lane4, col, half); break;
+    case 5: nib_rows<5>(lds, lane4, col, half); break;
+    case 6: nib_rows<6>(lds, lane4, col, half); break;
+    default: nib_rows<7>(lds, lane4, col, half); break;
+    }
+}
+
+__device__ __forceinline__ uint32_t nib_fold(const char *lds, uint32_t lane4, uint32_t s)
+{
+    const char *t = lds + kShiftOff + lane4;
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        v[j] = *reinterpret_cast<const uint32_t *>(t + (uint32_t) j * 4096u + ((s >> (4 * j)) & 15u) * 256u);
+    }
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
+}
+
 // Zero the bytes of a 16-byte block at virtual offset bs past the end v.
 __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t bs, uint32_t vlen)
 {
@@ -1353,7 +1405,8 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         table_entries<cx_xpow8n(kRow - kGran)>(__builtin_amdgcn_readfirstlane(idx >> 8), idx & 255u,
                                                tab_v[e], tab_sv[e]);
     }
-    write_tables(lds, tid, tab_v, tab_sv);
+    constexpr bool kNib = L64 && CIO_SMALL_NIBFOLD;
+    write_tables<false, !kNib>(lds, tid, tab_v, tab_sv);
     // The multiply by xl as a 32 x 32 GF(2) matrix held in registers: column
     // j = xl * x^(31 - j) (reflected bit j).
     uint32_t col[32];
@@ -1361,6 +1414,9 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
 #pragma unroll
     for (int j = 30; j >= 0; --j) {
         col[j] = (col[j + 1] >> 1) ^ (CIOA_POLY & (0u - (col[j + 1] & 1u)));
+    }
+    if (kNib) {
+        write_nib_tables(lds, tid, col);
     }
     // Uniform batch without seeds: the head granule's fix-up (clear the bytes
     // before the content, XOR the initial 0xffffffff in) is the same for every
@@ -1444,7 +1500,9 @@ crc32_small_kernel(const uint8_t *base, uint64_t ustride, uint64_t ua0, uint64_t
         issue(cur, c + CIO_SMALL_SLOTS);
         if (live) {
             uint32_t x = st;
-            if (!(CIO_SMALL_EXP & 1)) {
+            if (kNib && !(CIO_SMALL_EXP & 1)) {
+                x = nib_fold(lds, lane << 2, st);
+            } else if (!(CIO_SMALL_EXP & 1)) {
                 // 32 x (bit-field sign extend, fused and-xor)
                 x = col[0] & (0u - (st & 1u));
 #pragma unroll
@@ -1933,8 +1991,9 @@ const char *plan_build(PlanHost &ph, const uint64_t *offs, const uint64_t *lens,
     uint64_t S = 0, bytes = 0;
     for (size_t i = 0; i < n; i++) {
         ChunkDesc &d = ph.desc[i];
-        d.a = offs[i] & ~15ull;
-        d.h = (uint32_t) (offs[i] & 15u);
+        const uint64_t amask = lens[i] > (uint64_t) kStep ? (uint64_t) CIO_HEAD_ALIGN - 1 : 15ull;
+        d.a = offs[i] & ~amask;
+        d.h = (uint32_t) (offs[i] & amask);
         d.vlen = d.h + lens[i];
         d.g = S;
         const uint64_t ns = lens[i] >= 4 ? (d.vlen + kStep - 1) / kStep : 0;
@@ -2071,7 +2130,7 @@ void plan_uniform(cio_crc32_plan *p, const uint64_t *offs, const uint64_t *lens,
         return;
     }
     for (size_t i = 1; i < n; i++) {
-        if (lens[i] != lens[0] || offs[i] != offs[0] + i * stride) {
+        if (lens[i] != lens[0] || offs[i] != offs[0] + i * stride || ph.desc[i].h != ph.desc[0].h) {
             return;
         }
     }
