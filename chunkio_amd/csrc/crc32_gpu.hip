@@ -1916,8 +1916,11 @@ const char *cio_gpu_last_error(void)
 
 const char *cio_gpu_version(void)
 {
+#define CIO_STR2(x) #x
+#define CIO_STR(x) CIO_STR2(x)
     return "chunkio_amd crc32 v9 gfx950 stream(l64-lanes permlane-transpose issue-ahead<=64steps pre-shift prio-rotate "
-           "coalesced-nt division-free-start slice4-lds32x perm direct-whole preshifted-partials wg-lds-fold) "
+           "coalesced-nt division-free-start slice4-lds32x perm direct-whole preshifted-partials wg-lds-fold "
+           "head-align=" CIO_STR(CIO_HEAD_ALIGN) ") "
            "small(4x16B dpp-reduce bitop3-fold prio-rotate) "
            "host(nt-staging graduated-groups pread-bounce multi-device vpclmul-crc_update small-batch-route) "
            "sha1(2-schedule-waves 4-block-handover continuation)";

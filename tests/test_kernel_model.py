@@ -19,10 +19,20 @@ ROW = GRAN * WAVE
 INIT = 0xFFFFFFFF
 
 
-def plan(offs, lens, W):
+def head_align():
+    """The library's virtual-start alignment for chunks longer than one step
+    (CIO_HEAD_ALIGN, reported in cio_gpu_version: 16 or 128)."""
+    import re
+    import chunkio_amd
+    m = re.search(rb"head-align=(\d+)", chunkio_amd.lib().cio_gpu_version())
+    return int(m.group(1)) if m else 16
+
+
+def plan(offs, lens, W, align=None):
+    align = head_align() if align is None else align
     desc, S = [], 0
     for o, n in zip(offs, lens):
-        h = o & 15
+        h = o & ((align - 1) if n > STEP else 15)
         vlen = h + n
         ns = (vlen + STEP - 1) // STEP if n >= 4 else 0
         desc.append(dict(a=o - h, h=h, vlen=vlen, g=S, nsteps=ns))
@@ -52,8 +62,8 @@ def lane_block(buf, d, jj, q, lane, seed):
     return bstart, vb, blk
 
 
-def model(buf, offs, lens, seeds, W):
-    desc, S, wc = plan(offs, lens, W)
+def model(buf, offs, lens, seeds, W, align=None):
+    desc, S, wc = plan(offs, lens, W, align)
     partials = {}
     start = lambda w: (w * S) // W  # noqa: E731
     for w in range(W):
@@ -114,8 +124,9 @@ def model(buf, offs, lens, seeds, W):
     return out
 
 
+@pytest.mark.parametrize("align", [16, 128])
 @pytest.mark.parametrize("W", [1, 3, 8, 64])
-def test_model_matches_crc_update(W):
+def test_model_matches_crc_update(W, align):
     rng = np.random.default_rng(W)
     lens = [0, 1, 3, 4, 5, 63, 64, 65, 4095, 4096, 4097, 8200, 13000, 2, 9000, 0, 30000]
     offs, pos = [], 0
@@ -125,7 +136,7 @@ def test_model_matches_crc_update(W):
         pos += n
     buf = rng.integers(0, 256, pos + 32, dtype=np.uint8)
     seeds = [int(x) for x in rng.integers(0, 2 ** 32, len(lens))]
-    got = model(buf, offs, lens, seeds, W)
+    got = model(buf, offs, lens, seeds, W, align)
     want = [po.crc_update(s, buf[o:o + n]) for s, o, n in zip(seeds, offs, lens)]
     assert got == want
 
