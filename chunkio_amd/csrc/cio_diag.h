@@ -66,13 +66,16 @@
 #endif
 
 /* Alignment of a chunk's virtual start for chunks longer than one 4 KiB
- * step: 16 (shipped through round 4) or 128 (one L2 line).  At 128 every
- * 1 KiB row of such a chunk is line-aligned, so consecutive rows and steps
- * never share a line; the head (up to 127 bytes of the neighbour) is zeroed
- * in registers as the 16-byte head always was.  Chunks of at most one step
- * keep 16 (they stay on the small-chunk kernel). */
+ * step: 128 (one L2 line, shipped from round 5) or 16 (rounds 1-4).  At 128
+ * every 1 KiB row of such a chunk is line-aligned, so consecutive rows and
+ * steps never share a line; the head (up to 127 bytes of the neighbour) is
+ * zeroed in registers as the 16-byte head always was.  At 16, a chunk at an
+ * offset that is not a multiple of 128 re-fetched the line each step boundary
+ * shares (cfg3, 16-byte packed: 1.024x the algorithmic bytes; at 128:
+ * 1.0004x, profiles/r05/cfg3_traffic/).  Chunks of at most one step keep 16
+ * (they stay on the small-chunk kernel). */
 #ifndef CIO_HEAD_ALIGN
-#define CIO_HEAD_ALIGN 16
+#define CIO_HEAD_ALIGN 128
 #endif
 
 /* Small-chunk kernel, L64 layout (CIO_GPU_L64=1): the lane's final multiply by
