@@ -301,14 +301,17 @@ def host_threads(threads=None):
     return int(_lib.lib().cio_crc32_host_threads())
 
 
-def route(cpu_max=None, threads=None, reset=False):
+def route(cpu_max=None, threads=None, reset=False, split=None):
     """The chunk layer's host/GPU route (crc_route.c): reset=True drops earlier
-    settings; cpu_max (bytes, -1 = every batch on the host) and threads set
-    the threshold and the host thread count.  Returns (cpu_max, threads) in
-    effect."""
+    settings; cpu_max (bytes, -1 = every batch on the host, 0 = every batch on
+    the GPU alone) and threads set the threshold and the host thread count;
+    split turns the split route (a GPU-bound batch shared with the host) on or
+    off.  Returns (cpu_max, threads) in effect."""
     lib = _lib.lib()
     if reset:
         lib.cio_crc32_route_reset()
+    if split is not None:
+        lib.cio_crc32_set_split_route(1 if split else 0)
     if cpu_max is not None:
         lib.cio_crc32_set_cpu_max(ctypes.c_size_t(cpu_max).value)
     if threads is not None:

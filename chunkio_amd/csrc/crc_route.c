@@ -36,8 +36,11 @@
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <unistd.h>
 
 #include <crc32/crc32.h>
@@ -63,6 +66,7 @@ static const double kCpuMemGBps = 131.0;
 
 static size_t g_cpu_max;
 static int g_cpu_max_set;
+static int g_split = -1;          /* split route: -1 not set (environment), 0 / 1 */
 static int g_threads;
 static int g_threads_set;
 
@@ -145,6 +149,7 @@ void cio_crc32_route_reset(void)
 {
     __atomic_store_n(&g_cpu_max_set, 0, __ATOMIC_RELEASE);
     __atomic_store_n(&g_threads_set, 0, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_split, -1, __ATOMIC_RELEASE);
 }
 
 /* Distinct device ordinals in a *_multi device list (1 for the current device). */
@@ -177,6 +182,121 @@ static int route_to_cpu(const size_t *lens, size_t n, const int *devices, int nd
     return 1;
 }
 
+/* ---- split route --------------------------------------------------------
+ *
+ * A batch that goes to the GPU leaves the calling thread (and its
+ * cio_crc32_host_threads() host CRC threads) waiting on the pipeline.  With
+ * the split route on (default; CIOA_SPLIT_ROUTE=0 or cio_crc32_set_split_route
+ * (0) turn it off, and so does an explicit cio_crc32_set_cpu_max(0): "all on
+ * the GPU") the host takes a suffix of the batch at the same time: the
+ * GPU part runs on a helper thread (on the caller's device list, or its
+ * current device) while the caller CRCs its share with the host batch, sized
+ * so both finish together under the cost model:
+ *
+ *   B_host / r_host = F_gpu + (B - B_host) / (G r_gpu)
+ *
+ * with r_host the host rate of this source (memory: min(T x 36, 131) GB/s;
+ * files: min(T x 22, 131) GB/s, the pread path measured in bench.py's verify
+ * leg).  Whole chunks only: the suffix is the last chunks whose total stays
+ * within B_host.  Results are the same as either engine alone. */
+static const double kCpuThreadFdGBps = 22.0;
+
+int cio_crc32_split_route(void)
+{
+    const int v = __atomic_load_n(&g_split, __ATOMIC_ACQUIRE);
+    if (v >= 0) {
+        return v;
+    }
+    const char *r = getenv("CIOA_SPLIT_ROUTE");
+    return !(r && strcmp(r, "0") == 0);
+}
+
+void cio_crc32_set_split_route(int on)
+{
+    __atomic_store_n(&g_split, on ? 1 : 0, __ATOMIC_RELEASE);
+}
+
+/* First chunk of the host's suffix (n = no split). */
+static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int fd)
+{
+    size_t explicit_max;
+    if (!cio_crc32_split_route() || n < 2 || (explicit_cpu_max(&explicit_max) && explicit_max == 0)) {
+        return n;    /* (an explicit threshold of 0 means every byte on the GPU) */
+    }
+    const int t = cio_crc32_host_threads();
+    double r_host = t * (fd ? kCpuThreadFdGBps : kCpuThreadGBps);
+    if (r_host > kCpuMemGBps) {
+        r_host = kCpuMemGBps;
+    }
+    const double r_gpu = (ndev_distinct > 1 ? ndev_distinct : 1) * kGpuGBps;
+    double total = 0;
+    for (size_t i = 0; i < n; i++) {
+        total += (double) lens[i];
+    }
+    const double b_host = (kGpuFixedUs * 1e-6 + total / (r_gpu * 1e9)) / (1.0 / (r_host * 1e9) + 1.0 / (r_gpu * 1e9));
+    size_t k = n;
+    double acc = 0;
+    while (k > 1 && acc + (double) lens[k - 1] <= b_host) {
+        acc += (double) lens[--k];
+    }
+    return k;
+}
+
+struct gpu_part {
+    const void *const *bufs;
+    const int *fds;
+    const uint64_t *foffs;
+    const size_t *lens;
+    const uint32_t *seeds;
+    uint32_t *out;
+    size_t n;
+    const int *devices;
+    int ndev;
+    int rc;
+    char err[512];
+};
+
+static void *gpu_part_run(void *arg)
+{
+    struct gpu_part *g = (struct gpu_part *) arg;
+    g->rc = g->fds ? cio_crc32_batch_fd_multi(g->fds, g->foffs, g->lens, g->seeds, g->out, g->n, g->devices, g->ndev)
+                   : cio_crc32_batch_host_multi(g->bufs, g->lens, g->seeds, g->out, g->n, g->devices, g->ndev);
+    if (g->rc != CIO_OK) {
+        snprintf(g->err, sizeof(g->err), "%s", cio_gpu_last_error());
+    }
+    return NULL;
+}
+
+/* Chunks [0, k) on the GPU (helper thread), [k, n) on the host (this thread). */
+static int run_split(const void *const *bufs, const int *fds, const uint64_t *foffs, const size_t *lens,
+                     const uint32_t *seeds, uint32_t *out_raw, size_t n, size_t k, const int *devices, int ndev)
+{
+    int cur = -1;
+    if (!devices || ndev <= 0) {
+        /* the helper thread must use the caller's current device */
+        cur = cio_gpu_get_device();
+        if (cur < 0) {
+            return cioa_fail_msg("cioa_crc_route", "no current HIP device");
+        }
+        devices = &cur;
+        ndev = 1;
+    }
+    struct gpu_part g = {bufs, fds, foffs, lens, seeds, out_raw, k, devices, ndev, CIO_ERROR, {0}};
+    pthread_t th;
+    if (pthread_create(&th, NULL, gpu_part_run, &g) != 0) {
+        return cioa_fail_msg("cioa_crc_route", "pthread_create failed");
+    }
+    const int t = cio_crc32_host_threads();
+    const int rc_host = fds ? cio_crc32_batch_fd_cpu(fds + k, foffs + k, lens + k, seeds ? seeds + k : NULL,
+                                                     out_raw + k, n - k, t)
+                            : cio_crc32_batch_cpu(bufs + k, lens + k, seeds ? seeds + k : NULL, out_raw + k, n - k, t);
+    pthread_join(th, NULL);
+    if (g.rc != CIO_OK) {
+        return cioa_fail_msg("cioa_crc_route: GPU part", g.err);
+    }
+    return rc_host;
+}
+
 int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
                          size_t n, const int *devices, int ndev)
 {
@@ -184,6 +304,10 @@ int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint
         return CIO_OK;
     }
     if (!route_to_cpu(lens, n, devices, ndev)) {
+        const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 0);
+        if (k < n) {
+            return run_split(bufs, NULL, NULL, lens, seeds, out_raw, n, k, devices, ndev);
+        }
         return cio_crc32_batch_host_multi(bufs, lens, seeds, out_raw, n, devices, ndev);
     }
     return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
@@ -196,6 +320,10 @@ int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens,
         return CIO_OK;
     }
     if (!route_to_cpu(lens, n, devices, ndev)) {
+        const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 1);
+        if (k < n) {
+            return run_split(NULL, fds, foffs, lens, seeds, out_raw, n, k, devices, ndev);
+        }
         return cio_crc32_batch_fd_multi(fds, foffs, lens, seeds, out_raw, n, devices, ndev);
     }
     return cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads());

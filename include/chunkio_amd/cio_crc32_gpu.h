@@ -249,11 +249,17 @@ int  cio_crc32_batch_fd_cpu(const int *fds, const uint64_t *foffs, const size_t 
  * ~17 MB per device in the call's device list; with two or more host threads
  * the host's DRAM rate beats a PCIe link and every host-memory batch stays on
  * the CPU.  CIOA_CPU_CRC_MAX (bytes) or cio_crc32_set_cpu_max() override the
- * threshold, 0 sends everything to the GPU; CIOA_HOST_CRC_THREADS or
+ * threshold, 0 sends everything to the GPU alone (no split); CIOA_HOST_CRC_THREADS or
  * cio_crc32_set_host_threads() (1..64) set the thread count.  The
  * cio_crc32_batch_* entry points never route. */
 size_t cio_crc32_cpu_max(void);
 void   cio_crc32_set_cpu_max(size_t bytes);
+/* Split route (default on; CIOA_SPLIT_ROUTE=0 turns it off): a chunk-layer
+ * batch that goes to the GPU is shared with the host -- the GPU part on a
+ * helper thread, a suffix of whole chunks on the caller's host CRC threads at
+ * the same time, sized by the same cost model so both finish together. */
+int    cio_crc32_split_route(void);
+void   cio_crc32_set_split_route(int on);
 int    cio_crc32_host_threads(void);
 void   cio_crc32_set_host_threads(int threads);
 /* Drop what the two setters set (back to the environment / defaults). */

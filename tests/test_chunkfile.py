@@ -22,9 +22,12 @@ INIT = 0xFFFFFFFF
 # crossover.  Each chunk-layer test runs both ways: the host route in the CPU
 # suite, the GPU route under -m gpu.  Results must not depend on the route.
 # "host_mt" is the host route with 8 host CRC threads (cio_crc32_batch_cpu's
-# pool, crc_cpu_batch.c).
+# pool, crc_cpu_batch.c); "split" sends every batch of two or more chunks to
+# the split route (the first chunks on the GPU from a helper thread, the rest
+# on the calling thread's host CRC at the same time).
 ROUTES = [pytest.param("host", id="host"), pytest.param("host_mt", id="host_mt"),
-          pytest.param("gpu", marks=pytest.mark.gpu, id="gpu")]
+          pytest.param("gpu", marks=pytest.mark.gpu, id="gpu"),
+          pytest.param("split", marks=pytest.mark.gpu, id="split")]
 
 
 @pytest.fixture
@@ -33,6 +36,11 @@ def route(request):
     if request.param == "gpu":
         request.getfixturevalue("cuda")
         cio.route(reset=True, cpu_max=0)
+    elif request.param == "split":
+        # every batch of two or more chunks shared: the first chunks on the
+        # GPU (helper thread), the rest on the calling thread's host CRC
+        request.getfixturevalue("cuda")
+        cio.route(reset=True, cpu_max=1, threads=1, split=True)
     elif request.param == "host_mt":
         cio.route(reset=True, cpu_max=1 << 62, threads=8)
     else:
@@ -657,3 +665,45 @@ print("ok", t)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split()[-2:] == ["ok", "499500"], r.stdout
+
+
+@pytest.mark.gpu
+def test_split_route_shares_gpu_bound_batches_with_the_host(cuda, tmp_path, data400):
+    """Default routing (one host CRC thread): a verify batch above the
+    crossover goes to the GPU; with the split route (default on) the calling
+    thread CRCs a suffix of the files meanwhile, so the GPU stages fewer bytes,
+    and every status, error and CRC equals the GPU-alone and host-alone
+    results (crc_route.c run_split)."""
+    import shutil
+    import chunkio_amd as cio
+    n = 24                                           # 24 x 2 MB = 49 MB > the ~17 MB crossover
+    paths = [str(tmp_path / "s" / f"c{i:03d}") for i in range(n)]
+    c, _ = cf.ChunkFile.open(paths[0])
+    for _ in range(5):
+        c.write(data400)
+    c.sync()
+    c.close()
+    for p in paths[1:]:
+        shutil.copyfile(paths[0], p)
+    with open(paths[17], "r+b") as f:               # a file in the host's suffix
+        f.seek(24 + 999)
+        b = f.read(1)
+        f.seek(24 + 999)
+        f.write(bytes([b[0] ^ 1]))
+    region = n * (2 + 5 * len(data400))
+    res = {}
+    try:
+        for tag, kw in (("gpu", dict(split=False)), ("split", dict(split=True)), ("host", dict(cpu_max=-1))):
+            cio.route(reset=True, threads=1, **kw)
+            res[tag] = cf.verify_paths(paths)
+            if tag != "host":
+                res[tag + "_staged"] = cio.pipe_last_timing()["staged_bytes"]
+    finally:
+        cio.route(reset=True)
+    for tag in ("split", "host"):
+        for a, b in zip(res["gpu"], res[tag]):
+            np.testing.assert_array_equal(a, b, err_msg=tag)
+    st, er, cr = res["gpu"]
+    assert [i for i in range(n) if st[i] != cf.CIO_OK] == [17] and er[17] == cf.CIO_ERR_BAD_CHECKSUM
+    assert res["gpu_staged"] >= region
+    assert 0 < res["split_staged"] < res["gpu_staged"], (res["split_staged"], res["gpu_staged"])

@@ -32,7 +32,8 @@ with open(os.path.join(GDIR, "manifest.json")) as _f:
 CHUNKS = MANIFEST["chunks"]
 NAMES = [c["name"] for c in CHUNKS]
 
-ROUTES = [pytest.param("host", id="host"), pytest.param("gpu", marks=pytest.mark.gpu, id="gpu")]
+ROUTES = [pytest.param("host", id="host"), pytest.param("gpu", marks=pytest.mark.gpu, id="gpu"),
+          pytest.param("split", marks=pytest.mark.gpu, id="split")]
 
 
 @pytest.fixture
@@ -41,6 +42,11 @@ def route(request):
     if request.param == "gpu":
         request.getfixturevalue("cuda")
         cio.route(reset=True, cpu_max=0)
+    elif request.param == "split":
+        # every batch of two or more chunks shared: the first chunks on the
+        # GPU (helper thread), the rest on the calling thread's host CRC
+        request.getfixturevalue("cuda")
+        cio.route(reset=True, cpu_max=1, threads=1, split=True)
     else:
         cio.route(reset=True, cpu_max=1 << 62, threads=1)
     yield request.param
