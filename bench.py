@@ -1205,7 +1205,10 @@ def run_verify(args, rank, world, device, dist, compact=False):
         import chunkio_amd as cio
         host_route = {}
         try:
-            for tag, kw in (("threads_1", {"cpu_max": -1, "threads": 1}),
+            # `value` is the default route: GPU-bound batches split with the
+            # calling thread (crc_route.c); gpu_alone is the same call with
+            # the split route off (every CRC byte on the GPU).
+            for tag, kw in (("gpu_alone", {"split": False}), ("threads_1", {"cpu_max": -1, "threads": 1}),
                             (f"threads_{host_cpu_threads()}", {"threads": host_cpu_threads()})):
                 cio.route(reset=True, **kw)
                 cf.verify_paths(paths)
@@ -1221,7 +1224,8 @@ def run_verify(args, rank, world, device, dist, compact=False):
         finally:
             cio.route(reset=True)
         host_route["note"] = ("cio_verify_paths with the CRC batch routed to the library's host crc_update "
-                              "(cio_crc32_batch_fd_cpu: pread + VPCLMULQDQ folding) instead of the GPU")
+                              "(cio_crc32_batch_fd_cpu: pread + VPCLMULQDQ folding) instead of the GPU; "
+                              "gpu_alone: the GPU without the split route's host share")
         cpu = None
         if rank == 0 and not args.no_cpu:
             import mmap
