@@ -36,6 +36,10 @@ int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint
 int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens, const uint32_t *seeds,
                       uint32_t *out_raw, size_t n, const int *devices, int ndev);
 
+/* host_pipeline.hip: set the calling thread's cio_gpu_pipe_last_timing record
+ * (6 values, as that call returns them). */
+void cioa_pipe_timing_set(const double *v);
+
 uint32_t cio_crc32_shift(uint32_t raw_state, uint64_t nbytes);
 uint32_t cio_crc32_combine(uint32_t raw_a, uint32_t raw0_b, uint64_t len_b);
 

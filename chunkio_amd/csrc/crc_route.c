@@ -254,6 +254,7 @@ struct gpu_part {
     int ndev;
     int rc;
     char err[512];
+    double timing[6];
 };
 
 static void *gpu_part_run(void *arg)
@@ -263,6 +264,8 @@ static void *gpu_part_run(void *arg)
                    : cio_crc32_batch_host_multi(g->bufs, g->lens, g->seeds, g->out, g->n, g->devices, g->ndev);
     if (g->rc != CIO_OK) {
         snprintf(g->err, sizeof(g->err), "%s", cio_gpu_last_error());
+    } else {
+        (void) cio_gpu_pipe_last_timing(g->timing, 6);
     }
     return NULL;
 }
@@ -281,7 +284,7 @@ static int run_split(const void *const *bufs, const int *fds, const uint64_t *fo
         devices = &cur;
         ndev = 1;
     }
-    struct gpu_part g = {bufs, fds, foffs, lens, seeds, out_raw, k, devices, ndev, CIO_ERROR, {0}};
+    struct gpu_part g = {bufs, fds, foffs, lens, seeds, out_raw, k, devices, ndev, CIO_ERROR, {0}, {0}};
     pthread_t th;
     if (pthread_create(&th, NULL, gpu_part_run, &g) != 0) {
         return cioa_fail_msg("cioa_crc_route", "pthread_create failed");
@@ -294,6 +297,7 @@ static int run_split(const void *const *bufs, const int *fds, const uint64_t *fo
     if (g.rc != CIO_OK) {
         return cioa_fail_msg("cioa_crc_route: GPU part", g.err);
     }
+    cioa_pipe_timing_set(g.timing);
     return rc_host;
 }
 

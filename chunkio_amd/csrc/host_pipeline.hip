@@ -1217,6 +1217,22 @@ extern "C" double cioa_debug_h2d_gbps(const void *host, size_t bytes, int reps)
     return r;
 }
 
+// The split route (crc_route.c) runs the GPU part on a helper thread and
+// hands its record to the calling thread, so cio_gpu_pipe_last_timing there
+// reports that part.
+extern "C" void cioa_pipe_timing_set(const double *v)
+{
+    PipeTiming pt;
+    pt.total_ms = v[0];
+    pt.copy_ms = v[1];
+    pt.slot_wait_ms = v[2];
+    pt.plan_ms = v[3];
+    pt.groups = v[4];
+    pt.bytes = v[5];
+    pt.valid = true;
+    t_last_timing = pt;
+}
+
 extern "C" int cio_gpu_pipe_last_timing(double *out, int n)
 {
     if (!out || n <= 0) {
