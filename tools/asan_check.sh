@@ -69,8 +69,12 @@ host|gpu)
         # still quarantined when libamdhip64's destructors unload the runtime
         # trips its "device runtime unloaded" CHECK at exit (seen in r04ao).
         export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:quarantine_size_mb=0
-        for m in immediate deferred; do
-            CIOA_CPU_CRC_MAX=0 timeout -k 10 300 $BIN/test_chunk_api $DATA "$W" $m
+        # CIOA_CPU_CRC_MAX=0: every batch on the GPU alone; =1: every batch of
+        # two or more chunks on the split route (GPU helper thread + host)
+        for cm in 0 1; do
+            for m in immediate deferred; do
+                CIOA_CPU_CRC_MAX=$cm timeout -k 10 300 $BIN/test_chunk_api $DATA "$W" $m
+            done
         done
         timeout -k 10 300 $BIN/test_multi "$W"
     fi
@@ -108,8 +112,10 @@ tsan|tsan-gpu)
             CIOA_CPU_CRC_MAX=$((1 << 62)) CIOA_HOST_CRC_THREADS=8 \
                 timeout -k 10 900 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m | tail -1
         else
-            TSAN_OPTIONS=halt_on_error=1:suppressions=$PWD/tools/tsan_rocm.supp CIOA_CPU_CRC_MAX=0 \
-                timeout -k 10 300 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m
+            for cm in 0 1; do
+                TSAN_OPTIONS=halt_on_error=1:suppressions=$PWD/tools/tsan_rocm.supp CIOA_CPU_CRC_MAX=$cm \
+                    timeout -k 10 300 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m
+            done
         fi
     done
     if [ "$MODE" = tsan-gpu ]; then
