@@ -216,6 +216,15 @@ void cio_crc32_set_split_route(int on)
     __atomic_store_n(&g_split, on ? 1 : 0, __ATOMIC_RELEASE);
 }
 
+/* Diagnostic (CIOA_SPLIT_HOSTFAST=1, tools/split_probe.py): also split a
+ * batch the model sends to the host because T host threads outrun the GPU,
+ * giving the GPU the share the same equal-finish sizing assigns it. */
+static int split_hostfast(void)
+{
+    const char *r = getenv("CIOA_SPLIT_HOSTFAST");     /* (read per batch: a probe toggles it) */
+    return r && strcmp(r, "1") == 0;
+}
+
 /* First chunk of the host's suffix (n = no split). */
 static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int fd)
 {
@@ -238,6 +247,9 @@ static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int f
     double acc = 0;
     while (k > 1 && acc + (double) lens[k - 1] <= b_host) {
         acc += (double) lens[--k];
+    }
+    if (split_hostfast() && k == 1 && b_host >= total) {
+        return 0;      /* (diagnostic path) the model gives the GPU nothing */
     }
     return k;
 }
@@ -301,14 +313,26 @@ static int run_split(const void *const *bufs, const int *fds, const uint64_t *fo
     return rc_host;
 }
 
+static int route_to_cpu_split(const size_t *lens, size_t n, const int *devices, int ndev)
+{
+    size_t m;
+    if (split_hostfast() && !explicit_cpu_max(&m) && cio_crc32_host_threads() > 1) {
+        return 0;
+    }
+    return route_to_cpu(lens, n, devices, ndev);
+}
+
 int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
                          size_t n, const int *devices, int ndev)
 {
     if (n == 0) {
         return CIO_OK;
     }
-    if (!route_to_cpu(lens, n, devices, ndev)) {
+    if (!route_to_cpu_split(lens, n, devices, ndev)) {
         const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 0);
+        if (k == 0) {
+            return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
+        }
         if (k < n) {
             return run_split(bufs, NULL, NULL, lens, seeds, out_raw, n, k, devices, ndev);
         }
@@ -323,8 +347,11 @@ int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens,
     if (n == 0) {
         return CIO_OK;
     }
-    if (!route_to_cpu(lens, n, devices, ndev)) {
+    if (!route_to_cpu_split(lens, n, devices, ndev)) {
         const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 1);
+        if (k == 0) {
+            return cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads());
+        }
         if (k < n) {
             return run_split(NULL, fds, foffs, lens, seeds, out_raw, n, k, devices, ndev);
         }
