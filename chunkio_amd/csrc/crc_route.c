@@ -41,6 +41,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <crc32/crc32.h>
@@ -302,10 +303,24 @@ static int run_split(const void *const *bufs, const int *fds, const uint64_t *fo
         return cioa_fail_msg("cioa_crc_route", "pthread_create failed");
     }
     const int t = cio_crc32_host_threads();
+    struct timespec t0, t1, t2;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     const int rc_host = fds ? cio_crc32_batch_fd_cpu(fds + k, foffs + k, lens + k, seeds ? seeds + k : NULL,
                                                      out_raw + k, n - k, t)
                             : cio_crc32_batch_cpu(bufs + k, lens + k, seeds ? seeds + k : NULL, out_raw + k, n - k, t);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
     pthread_join(th, NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t2);
+    if (getenv("CIOA_ROUTE_DEBUG")) {
+        double hb = 0, gb = 0;
+        for (size_t i = 0; i < n; i++) {
+            *(i < k ? &gb : &hb) += (double) lens[i];
+        }
+        fprintf(stderr, "split route: %zu chunks, gpu %zu (%.1f MB), host %zu (%.1f MB, %d threads): "
+                        "host done %.2f ms, gpu done %.2f ms\n", n, k, gb / 1e6, n - k, hb / 1e6, t,
+                (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) / 1e6,
+                (t2.tv_sec - t0.tv_sec) * 1e3 + (t2.tv_nsec - t0.tv_nsec) / 1e6);
+    }
     if (g.rc != CIO_OK) {
         return cioa_fail_msg("cioa_crc_route: GPU part", g.err);
     }

@@ -23,6 +23,10 @@ sys.path.insert(0, ROOT)
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     import chunkio_amd as cio
+    if os.environ.get("SPLIT_PROBE_BIND") == "1":
+        # as bench.py's host legs do: this process on the GPU's NUMA node
+        import bench
+        print("bound to", bench.bind_to_gpu_node(0), "CPUs", flush=True)
     from chunkio_amd import chunkfile as cf
     d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8).tobytes()
     root = tempfile.mkdtemp(prefix="cioa-split-")
