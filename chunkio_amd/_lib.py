@@ -25,7 +25,7 @@ EXPORTS = (
     "cio_crc32_batch_host_multi", "cio_crc32_split_host_multi", "cio_crc32_batch_fd_multi", "cio_gpu_device_count", "cio_gpu_set_device", "cio_gpu_get_device", "cio_gpu_numa_node",
     "cio_gpu_pci_bus_id", "cio_gpu_plan_cache_stats",
     "cio_crc32_host_register", "cio_crc32_host_unregister", "cio_gpu_pipe_last_timing",
-    "cio_crc32_cpu_max", "cio_crc32_set_cpu_max", "cio_crc32_split_route", "cio_crc32_set_split_route", "cio_crc32_host_threads", "cio_crc32_set_host_threads",
+    "cio_crc32_cpu_max", "cio_crc32_set_cpu_max", "cio_crc32_split_route", "cio_crc32_set_split_route", "cio_crc32_split_rates", "cio_crc32_split_forget", "cio_crc32_host_threads", "cio_crc32_set_host_threads",
     "cio_crc32_route_reset",
     "cio_crc32_batch_cpu", "cio_crc32_batch_fd_cpu",
     "cio_gpu_fill_synthetic", "cio_sha1_batch_dev", "cio_sha1_batch_dev_async",
@@ -98,6 +98,8 @@ def _bind(lib):
         "cio_crc32_set_cpu_max": (None, [ctypes.c_size_t]),
         "cio_crc32_split_route": (ctypes.c_int, []),
         "cio_crc32_set_split_route": (None, [ctypes.c_int]),
+        "cio_crc32_split_rates": (None, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+        "cio_crc32_split_forget": (None, []),
         "cio_crc32_host_threads": (ctypes.c_int, []),
         "cio_crc32_set_host_threads": (None, [ctypes.c_int]),
         "cio_crc32_route_reset": (None, []),

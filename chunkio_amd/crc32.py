@@ -311,12 +311,24 @@ def route(cpu_max=None, threads=None, reset=False, split=None):
     if reset:
         lib.cio_crc32_route_reset()
     if split is not None:
-        lib.cio_crc32_set_split_route(1 if split else 0)
+        lib.cio_crc32_set_split_route(2 if split == "force" else 1 if split else 0)
     if cpu_max is not None:
         lib.cio_crc32_set_cpu_max(ctypes.c_size_t(cpu_max).value)
     if threads is not None:
         lib.cio_crc32_set_host_threads(int(threads))
     return int(lib.cio_crc32_cpu_max()), int(lib.cio_crc32_host_threads())
+
+
+def split_rates(forget=False):
+    """The rates (GB/s) the split route sizes its next split with
+    (cio_crc32_split_rates); forget=True drops the learned ones first."""
+    lib = _lib.lib()
+    if forget:
+        lib.cio_crc32_split_forget()
+    v = (ctypes.c_double * 6)()
+    lib.cio_crc32_split_rates(v, 6)
+    return dict(zip(("host_mem_t1", "host_fd_t1", "host_mem_t", "host_fd_t", "gpu_mem", "gpu_fd"),
+                    (round(x, 2) for x in v)))
 
 
 def device_count():

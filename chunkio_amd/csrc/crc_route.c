@@ -185,22 +185,34 @@ static int route_to_cpu(const size_t *lens, size_t n, const int *devices, int nd
 
 /* ---- split route --------------------------------------------------------
  *
- * A batch that goes to the GPU leaves the calling thread (and its
- * cio_crc32_host_threads() host CRC threads) waiting on the pipeline.  With
- * the split route on (default; CIOA_SPLIT_ROUTE=0 or cio_crc32_set_split_route
- * (0) turn it off, and so does an explicit cio_crc32_set_cpu_max(0): "all on
- * the GPU") the host takes a suffix of the batch at the same time: the
- * GPU part runs on a helper thread (on the caller's device list, or its
- * current device) while the caller CRCs its share with the host batch, sized
- * so both finish together under the cost model:
+ * Both engines at once.  With the split route on (default; CIOA_SPLIT_ROUTE=0
+ * or cio_crc32_set_split_route(0) turn it off, and so does any explicit
+ * threshold -- cio_crc32_set_cpu_max / CIOA_CPU_CRC_MAX: the caller chose an
+ * engine) a large batch runs on the GPU and on the host at the same time: the
+ * GPU part (the first chunks) on a helper thread, on the caller's device list
+ * or its current device, and a suffix of whole chunks on the caller's
+ * cio_crc32_host_threads() host threads, sized so both finish together:
  *
  *   B_host / r_host = F_gpu + (B - B_host) / (G r_gpu)
  *
- * with r_host the host rate of this source (memory: min(T x 36, 131) GB/s;
- * files: min(T x 22, 131) GB/s, the pread path measured in bench.py's verify
- * leg).  Whole chunks only: the suffix is the last chunks whose total stays
- * within B_host.  Results are the same as either engine alone. */
+ * The rates are learned: every split measures the host part's rate and the
+ * GPU part's rate *while the other engine runs* (the GPU path's copy and
+ * pread threads share the host's cores and memory with the CRC threads, so
+ * the concurrent rates are not the solo ones), per host thread count and
+ * source (memory / file), and the next split of that kind is sized with their
+ * running average.  The first split of a kind starts from the model (memory
+ * min(T x 36, 131) GB/s, files min(T x 22, 131) GB/s, GPU 54.7 GB/s per
+ * device).  A split is taken when it gives the GPU at least kMinGpuShare
+ * bytes and is predicted to finish before the better engine alone; this
+ * covers batches the threshold sends to the GPU (one host thread: the caller
+ * joins in) and batches it keeps on the host (T threads outrun one PCIe link,
+ * and the GPU adds its share).  Results are the same as either engine alone.
+ * Measured on the 1000 perf files (profiles/r05/split_probe_*.txt). */
 static const double kCpuThreadFdGBps = 22.0;
+static const double kMinGpuShare = 32e6;
+enum { kMaxT = 64 };
+static double g_rh[2][kMaxT + 1];        /* learned host rate in a split, GB/s (0: none yet) */
+static double g_rg[2];                   /* learned GPU rate per device in a split, GB/s */
 
 int cio_crc32_split_route(void)
 {
@@ -214,43 +226,113 @@ int cio_crc32_split_route(void)
 
 void cio_crc32_set_split_route(int on)
 {
-    __atomic_store_n(&g_split, on ? 1 : 0, __ATOMIC_RELEASE);
+    /* 0 off, 1 on, 2 forced: every batch of two or more chunks split, the
+     * GPU taking at least its first chunk (tests) */
+    __atomic_store_n(&g_split, on == 2 ? 2 : on ? 1 : 0, __ATOMIC_RELEASE);
 }
 
-/* Diagnostic (CIOA_SPLIT_HOSTFAST=1, tools/split_probe.py): also split a
- * batch the model sends to the host because T host threads outrun the GPU,
- * giving the GPU the share the same equal-finish sizing assigns it. */
-static int split_hostfast(void)
+static double ld_rate(const double *p)
 {
-    const char *r = getenv("CIOA_SPLIT_HOSTFAST");     /* (read per batch: a probe toggles it) */
-    return r && strcmp(r, "1") == 0;
+    double v;
+    __atomic_load(p, &v, __ATOMIC_RELAXED);
+    return v;
 }
 
-/* First chunk of the host's suffix (n = no split). */
-static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int fd)
+static void learn(double *p, double x)
+{
+    const double old = ld_rate(p);
+    const double v = old > 0 ? 0.5 * old + 0.5 * x : x;
+    __atomic_store(p, &v, __ATOMIC_RELAXED);
+}
+
+static double host_rate(int t, int fd)
+{
+    const double l = ld_rate(&g_rh[fd][t]);
+    if (l > 0) {
+        return l;
+    }
+    const double m = t * (fd ? kCpuThreadFdGBps : kCpuThreadGBps);
+    return m < kCpuMemGBps ? m : kCpuMemGBps;
+}
+
+static double gpu_rate(int fd)
+{
+    const double l = ld_rate(&g_rg[fd]);
+    return l > 0 ? l : kGpuGBps;
+}
+
+void cio_crc32_split_rates(double *out, int n)
+{
+    /* {host mem T=1, host fd T=1, host mem T, host fd T, gpu mem, gpu fd} for
+     * T = cio_crc32_host_threads(): what the next split would be sized with */
+    const int t = cio_crc32_host_threads();
+    const double v[6] = {host_rate(1, 0), host_rate(1, 1), host_rate(t, 0), host_rate(t, 1), gpu_rate(0), gpu_rate(1)};
+    for (int i = 0; i < n && i < 6; i++) {
+        out[i] = v[i];
+    }
+}
+
+void cio_crc32_split_forget(void)
+{
+    const double z = 0;
+    for (int f = 0; f < 2; f++) {
+        for (int t = 0; t <= kMaxT; t++) {
+            __atomic_store(&g_rh[f][t], &z, __ATOMIC_RELAXED);
+        }
+        __atomic_store(&g_rg[f], &z, __ATOMIC_RELAXED);
+    }
+}
+
+/* Whether a GPU is visible (checked once; a host-routed batch is only shared
+ * with one that exists). */
+static int gpu_present(void)
+{
+    static int v = -1;
+    int x = __atomic_load_n(&v, __ATOMIC_ACQUIRE);
+    if (x < 0) {
+        x = cio_gpu_device_count() > 0;
+        __atomic_store_n(&v, x, __ATOMIC_RELEASE);
+    }
+    return x;
+}
+
+/* The GPU prefix of a split: chunks [0, k) on the GPU, [k, n) on the host;
+ * k == n: the GPU alone, k == 0: the host alone. */
+static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int fd, int gpu_bound)
 {
     size_t explicit_max;
-    if (!cio_crc32_split_route() || n < 2 || (explicit_cpu_max(&explicit_max) && explicit_max == 0)) {
-        return n;    /* (an explicit threshold of 0 means every byte on the GPU) */
+    const int mode = cio_crc32_split_route();
+    const int have_max = explicit_cpu_max(&explicit_max);
+    if (mode == 0 || n < 2 || (have_max && explicit_max == 0)) {
+        return gpu_bound ? n : 0;      /* (an explicit threshold of 0: the GPU alone) */
+    }
+    if (!gpu_bound && !gpu_present()) {
+        return 0;                      /* host-routed, and no GPU to share with */
+    }
+    if (mode != 2 && have_max && !(gpu_bound && __atomic_load_n(&g_split, __ATOMIC_ACQUIRE) == 1)) {
+        /* an explicit threshold picks one engine, unless the caller also
+         * turned the split on: then a batch the threshold sends to the GPU
+         * may still be shared */
+        return gpu_bound ? n : 0;
     }
     const int t = cio_crc32_host_threads();
-    double r_host = t * (fd ? kCpuThreadFdGBps : kCpuThreadGBps);
-    if (r_host > kCpuMemGBps) {
-        r_host = kCpuMemGBps;
-    }
-    const double r_gpu = (ndev_distinct > 1 ? ndev_distinct : 1) * kGpuGBps;
+    const double r_host = host_rate(t, fd) * 1e9;
+    const double r_gpu = (ndev_distinct > 1 ? ndev_distinct : 1) * gpu_rate(fd) * 1e9;
+    const double f = kGpuFixedUs * 1e-6;
     double total = 0;
     for (size_t i = 0; i < n; i++) {
         total += (double) lens[i];
     }
-    const double b_host = (kGpuFixedUs * 1e-6 + total / (r_gpu * 1e9)) / (1.0 / (r_host * 1e9) + 1.0 / (r_gpu * 1e9));
+    const double b_host = (f + total / r_gpu) / (1.0 / r_host + 1.0 / r_gpu);
+    const double t_split = b_host / r_host;
+    const double t_alone = gpu_bound ? f + total / r_gpu : total / r_host;
+    if (mode != 2 && (total - b_host < kMinGpuShare || t_split >= t_alone)) {
+        return gpu_bound ? n : 0;
+    }
     size_t k = n;
     double acc = 0;
     while (k > 1 && acc + (double) lens[k - 1] <= b_host) {
         acc += (double) lens[--k];
-    }
-    if (split_hostfast() && k == 1 && b_host >= total) {
-        return 0;      /* (diagnostic path) the model gives the GPU nothing */
     }
     return k;
 }
@@ -266,15 +348,25 @@ struct gpu_part {
     const int *devices;
     int ndev;
     int rc;
+    double secs;
     char err[512];
     double timing[6];
 };
 
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + (double) ts.tv_nsec * 1e-9;
+}
+
 static void *gpu_part_run(void *arg)
 {
     struct gpu_part *g = (struct gpu_part *) arg;
+    const double t0 = now_s();
     g->rc = g->fds ? cio_crc32_batch_fd_multi(g->fds, g->foffs, g->lens, g->seeds, g->out, g->n, g->devices, g->ndev)
                    : cio_crc32_batch_host_multi(g->bufs, g->lens, g->seeds, g->out, g->n, g->devices, g->ndev);
+    g->secs = now_s() - t0;
     if (g->rc != CIO_OK) {
         snprintf(g->err, sizeof(g->err), "%s", cio_gpu_last_error());
     } else {
@@ -283,58 +375,67 @@ static void *gpu_part_run(void *arg)
     return NULL;
 }
 
-/* Chunks [0, k) on the GPU (helper thread), [k, n) on the host (this thread). */
+/* Chunks [0, k) on the GPU (helper thread), [k, n) on the host (this thread).
+ * host_routed: the threshold had put the whole batch on the host, so a GPU
+ * part that fails is redone on the host instead of failing the batch. */
 static int run_split(const void *const *bufs, const int *fds, const uint64_t *foffs, const size_t *lens,
-                     const uint32_t *seeds, uint32_t *out_raw, size_t n, size_t k, const int *devices, int ndev)
+                     const uint32_t *seeds, uint32_t *out_raw, size_t n, size_t k, const int *devices, int ndev,
+                     int host_routed)
 {
     int cur = -1;
+    const int gdev = devices ? distinct_devices(devices, ndev) : 1;
     if (!devices || ndev <= 0) {
         /* the helper thread must use the caller's current device */
         cur = cio_gpu_get_device();
         if (cur < 0) {
+            if (host_routed) {
+                return fds ? cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads())
+                           : cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
+            }
             return cioa_fail_msg("cioa_crc_route", "no current HIP device");
         }
         devices = &cur;
         ndev = 1;
     }
-    struct gpu_part g = {bufs, fds, foffs, lens, seeds, out_raw, k, devices, ndev, CIO_ERROR, {0}, {0}};
+    struct gpu_part g = {bufs, fds, foffs, lens, seeds, out_raw, k, devices, ndev, CIO_ERROR, 0, {0}, {0}};
     pthread_t th;
     if (pthread_create(&th, NULL, gpu_part_run, &g) != 0) {
         return cioa_fail_msg("cioa_crc_route", "pthread_create failed");
     }
     const int t = cio_crc32_host_threads();
-    struct timespec t0, t1, t2;
-    clock_gettime(CLOCK_MONOTONIC, &t0);
+    const double t0 = now_s();
     const int rc_host = fds ? cio_crc32_batch_fd_cpu(fds + k, foffs + k, lens + k, seeds ? seeds + k : NULL,
                                                      out_raw + k, n - k, t)
                             : cio_crc32_batch_cpu(bufs + k, lens + k, seeds ? seeds + k : NULL, out_raw + k, n - k, t);
-    clock_gettime(CLOCK_MONOTONIC, &t1);
+    const double t_host = now_s() - t0;
     pthread_join(th, NULL);
-    clock_gettime(CLOCK_MONOTONIC, &t2);
-    if (getenv("CIOA_ROUTE_DEBUG")) {
-        double hb = 0, gb = 0;
-        for (size_t i = 0; i < n; i++) {
-            *(i < k ? &gb : &hb) += (double) lens[i];
-        }
-        fprintf(stderr, "split route: %zu chunks, gpu %zu (%.1f MB), host %zu (%.1f MB, %d threads): "
-                        "host done %.2f ms, gpu done %.2f ms\n", n, k, gb / 1e6, n - k, hb / 1e6, t,
-                (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) / 1e6,
-                (t2.tv_sec - t0.tv_sec) * 1e3 + (t2.tv_nsec - t0.tv_nsec) / 1e6);
-    }
     if (g.rc != CIO_OK) {
+        if (host_routed && rc_host == CIO_OK) {
+            /* redo the GPU's share where the threshold had put it */
+            return fds ? cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, k, t)
+                       : cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, k, t);
+        }
         return cioa_fail_msg("cioa_crc_route: GPU part", g.err);
+    }
+    double hb = 0, gb = 0;
+    for (size_t i = 0; i < n; i++) {
+        *(i < k ? &gb : &hb) += (double) lens[i];
+    }
+    const int fd = fds != NULL;
+    if (rc_host == CIO_OK && hb >= 8e6 && t_host > 0) {
+        learn(&g_rh[fd][t], hb / t_host / 1e9);
+    }
+    const double tg = g.secs - kGpuFixedUs * 1e-6;
+    if (gb >= 8e6 && tg > 0.5 * g.secs) {
+        learn(&g_rg[fd], gb / tg / 1e9 / gdev);
+    }
+    if (getenv("CIOA_ROUTE_DEBUG")) {
+        fprintf(stderr, "split route: %zu chunks, gpu %zu (%.1f MB), host %zu (%.1f MB, %d threads): "
+                        "host %.2f ms, gpu %.2f ms; next: host %.1f GB/s, gpu %.1f GB/s\n", n, k, gb / 1e6, n - k,
+                hb / 1e6, t, t_host * 1e3, g.secs * 1e3, host_rate(t, fd), gpu_rate(fd));
     }
     cioa_pipe_timing_set(g.timing);
     return rc_host;
-}
-
-static int route_to_cpu_split(const size_t *lens, size_t n, const int *devices, int ndev)
-{
-    size_t m;
-    if (split_hostfast() && !explicit_cpu_max(&m) && cio_crc32_host_threads() > 1) {
-        return 0;
-    }
-    return route_to_cpu(lens, n, devices, ndev);
 }
 
 int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
@@ -343,17 +444,15 @@ int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint
     if (n == 0) {
         return CIO_OK;
     }
-    if (!route_to_cpu_split(lens, n, devices, ndev)) {
-        const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 0);
-        if (k == 0) {
-            return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
-        }
-        if (k < n) {
-            return run_split(bufs, NULL, NULL, lens, seeds, out_raw, n, k, devices, ndev);
-        }
-        return cio_crc32_batch_host_multi(bufs, lens, seeds, out_raw, n, devices, ndev);
+    const int gpu_bound = !route_to_cpu(lens, n, devices, ndev);
+    const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 0, gpu_bound);
+    if (k == 0) {
+        return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
     }
-    return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
+    if (k < n) {
+        return run_split(bufs, NULL, NULL, lens, seeds, out_raw, n, k, devices, ndev, !gpu_bound);
+    }
+    return cio_crc32_batch_host_multi(bufs, lens, seeds, out_raw, n, devices, ndev);
 }
 
 int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens, const uint32_t *seeds,
@@ -362,15 +461,13 @@ int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens,
     if (n == 0) {
         return CIO_OK;
     }
-    if (!route_to_cpu_split(lens, n, devices, ndev)) {
-        const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 1);
-        if (k == 0) {
-            return cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads());
-        }
-        if (k < n) {
-            return run_split(NULL, fds, foffs, lens, seeds, out_raw, n, k, devices, ndev);
-        }
-        return cio_crc32_batch_fd_multi(fds, foffs, lens, seeds, out_raw, n, devices, ndev);
+    const int gpu_bound = !route_to_cpu(lens, n, devices, ndev);
+    const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 1, gpu_bound);
+    if (k == 0) {
+        return cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads());
     }
-    return cio_crc32_batch_fd_cpu(fds, foffs, lens, seeds, out_raw, n, cio_crc32_host_threads());
+    if (k < n) {
+        return run_split(NULL, fds, foffs, lens, seeds, out_raw, n, k, devices, ndev, !gpu_bound);
+    }
+    return cio_crc32_batch_fd_multi(fds, foffs, lens, seeds, out_raw, n, devices, ndev);
 }

@@ -254,12 +254,23 @@ int  cio_crc32_batch_fd_cpu(const int *fds, const uint64_t *foffs, const size_t 
  * cio_crc32_batch_* entry points never route. */
 size_t cio_crc32_cpu_max(void);
 void   cio_crc32_set_cpu_max(size_t bytes);
-/* Split route (default on; CIOA_SPLIT_ROUTE=0 turns it off): a chunk-layer
- * batch that goes to the GPU is shared with the host -- the GPU part on a
- * helper thread, a suffix of whole chunks on the caller's host CRC threads at
- * the same time, sized by the same cost model so both finish together. */
+/* Split route (default on; CIOA_SPLIT_ROUTE=0 or set_split_route(0) turn it
+ * off): a large chunk-layer batch runs on the GPU and the host at once -- the
+ * GPU part (first chunks) on a helper thread, a suffix of whole chunks on the
+ * caller's host CRC threads -- sized so both finish together with rates
+ * learned from earlier splits (crc_route.c).  Taken when it gives the GPU at
+ * least 32 MB and beats the better engine alone, both for batches the
+ * threshold sends to the GPU and for batches it keeps on the host.  An
+ * explicit threshold (cio_crc32_set_cpu_max / CIOA_CPU_CRC_MAX) picks one
+ * engine unless set_split_route(1) was also called; 0 is always the GPU
+ * alone.  set_split_route(2) forces a split of every batch of 2+ chunks
+ * (tests).  split_rates: {host memory T=1, host file T=1, host memory T,
+ * host file T, GPU memory, GPU file} GB/s the next split is sized with, T =
+ * cio_crc32_host_threads(); split_forget drops what was learned. */
 int    cio_crc32_split_route(void);
 void   cio_crc32_set_split_route(int on);
+void   cio_crc32_split_rates(double *out, int n);
+void   cio_crc32_split_forget(void);
 int    cio_crc32_host_threads(void);
 void   cio_crc32_set_host_threads(int threads);
 /* Drop what the two setters set (back to the environment / defaults). */

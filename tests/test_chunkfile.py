@@ -40,7 +40,7 @@ def route(request):
         # every batch of two or more chunks shared: the first chunks on the
         # GPU (helper thread), the rest on the calling thread's host CRC
         request.getfixturevalue("cuda")
-        cio.route(reset=True, cpu_max=1, threads=1, split=True)
+        cio.route(reset=True, cpu_max=1, threads=1, split="force")
     elif request.param == "host_mt":
         cio.route(reset=True, cpu_max=1 << 62, threads=8)
     else:
@@ -676,7 +676,7 @@ def test_split_route_shares_gpu_bound_batches_with_the_host(cuda, tmp_path, data
     results (crc_route.c run_split)."""
     import shutil
     import chunkio_amd as cio
-    n = 24                                           # 24 x 2 MB = 49 MB > the ~17 MB crossover
+    n = 48                                           # 48 x 2 MB = 98 MB > the ~17 MB crossover
     paths = [str(tmp_path / "s" / f"c{i:03d}") for i in range(n)]
     c, _ = cf.ChunkFile.open(paths[0])
     for _ in range(5):
@@ -685,7 +685,7 @@ def test_split_route_shares_gpu_bound_batches_with_the_host(cuda, tmp_path, data
     c.close()
     for p in paths[1:]:
         shutil.copyfile(paths[0], p)
-    with open(paths[17], "r+b") as f:               # a file in the host's suffix
+    with open(paths[40], "r+b") as f:               # a file in the host's suffix
         f.seek(24 + 999)
         b = f.read(1)
         f.seek(24 + 999)
@@ -704,6 +704,78 @@ def test_split_route_shares_gpu_bound_batches_with_the_host(cuda, tmp_path, data
         for a, b in zip(res["gpu"], res[tag]):
             np.testing.assert_array_equal(a, b, err_msg=tag)
     st, er, cr = res["gpu"]
-    assert [i for i in range(n) if st[i] != cf.CIO_OK] == [17] and er[17] == cf.CIO_ERR_BAD_CHECKSUM
+    assert [i for i in range(n) if st[i] != cf.CIO_OK] == [40] and er[40] == cf.CIO_ERR_BAD_CHECKSUM
     assert res["gpu_staged"] >= region
     assert 0 < res["split_staged"] < res["gpu_staged"], (res["split_staged"], res["gpu_staged"])
+
+
+def test_default_route_stays_on_the_host_without_a_gpu(tmp_path, data400):
+    """With host threads granted and no explicit threshold, a large batch is a
+    candidate for the split route's GPU share; on a machine without a GPU (this
+    CPU suite) it must stay whole on the host and succeed."""
+    import shutil
+    import chunkio_amd as cio
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    n = 24                                           # 49 MB: above the split's 32 MB minimum GPU share
+    paths = [str(tmp_path / "s" / f"c{i:03d}") for i in range(n)]
+    cio.route(reset=True, cpu_max=-1)
+    try:
+        c, _ = cf.ChunkFile.open(paths[0])
+        for _ in range(5):
+            c.write(data400)
+        c.sync()
+        c.close()
+        for p in paths[1:]:
+            shutil.copyfile(paths[0], p)
+        cio.route(reset=True, threads=8)
+        st, er, cr = cf.verify_paths(paths)
+    finally:
+        cio.route(reset=True)
+    assert list(st) == [cf.CIO_OK] * n
+    assert all((int(x) ^ 0xFFFFFFFF) == 0x088740E7 for x in cr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 4])
+def test_split_route_learns_rates_and_matches_either_engine(cuda, tmp_path, data400, threads):
+    """The split route sizes each split with rates learned from the previous
+    ones (cio_crc32_split_rates): after a few verify calls over 200 files
+    (400 MB) the learned host and GPU rates differ from the model's, every
+    call returns the host-alone results, and with 4 host threads -- where the
+    threshold keeps the batch on the host -- the GPU still takes a share."""
+    import shutil
+    import chunkio_amd as cio
+    n = 200
+    paths = [str(tmp_path / "s" / f"c{i:03d}") for i in range(n)]
+    c, _ = cf.ChunkFile.open(paths[0])
+    for _ in range(5):
+        c.write(data400)
+    c.sync()
+    c.close()
+    for p in paths[1:]:
+        shutil.copyfile(paths[0], p)
+    with open(paths[123], "r+b") as f:
+        f.seek(24 + 5)
+        f.write(b"#")
+    try:
+        cio.route(reset=True, cpu_max=-1, threads=threads)
+        want = cf.verify_paths(paths)
+        cio.route(reset=True, threads=threads)
+        model = cio.split_rates(forget=True)
+        for _ in range(4):
+            got = cf.verify_paths(paths)
+            for a, b in zip(got, want):
+                np.testing.assert_array_equal(a, b)
+            staged = cio.pipe_last_timing()["staged_bytes"]
+            assert 0 < staged < n * (2 + 5 * len(data400)), staged
+        learned = cio.split_rates()
+    finally:
+        cio.route(reset=True)
+        cio.split_rates(forget=True)
+    key = "host_fd_t1" if threads == 1 else "host_fd_t"
+    assert learned[key] != model[key] and learned["gpu_fd"] != model["gpu_fd"], (model, learned)

@@ -46,7 +46,7 @@ def route(request):
         # every batch of two or more chunks shared: the first chunks on the
         # GPU (helper thread), the rest on the calling thread's host CRC
         request.getfixturevalue("cuda")
-        cio.route(reset=True, cpu_max=1, threads=1, split=True)
+        cio.route(reset=True, cpu_max=1, threads=1, split="force")
     else:
         cio.route(reset=True, cpu_max=1 << 62, threads=1)
     yield request.param
