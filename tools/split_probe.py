@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
 """Verify-on-load of 1000 perf-test chunk files (2 MB each, page cache) by one
 cio_verify_paths call per route setting, interleaved over rounds: the host
-alone, the GPU alone, and the split route at several host thread counts, plus
-the diagnostic split of batches the model gives the host entirely
-(CIOA_SPLIT_HOSTFAST=1).  Prints GB/s per setting (min time per round,
+alone, the GPU alone, and the default route (the split route, rates learned
+over the calls) at several host thread counts.  Prints GB/s per setting (min time per round,
 median over rounds) and checks that every setting returns the same results.
 
     python tools/split_probe.py [rounds]
@@ -43,19 +42,18 @@ def main():
         region = files * (2 + 5 * len(d400))
         settings = [("host T=1", dict(cpu_max=-1, threads=1), "0"),
                     ("gpu alone", dict(threads=1, split=False), "0"),
-                    ("split T=1", dict(threads=1, split=True), "0"),
+                    ("default T=1 (split)", dict(threads=1), "0"),
                     ("host T=4", dict(cpu_max=-1, threads=4), "0"),
-                    ("split T=4 (hostfast)", dict(threads=4, split=True), "1"),
+                    ("default T=4 (split)", dict(threads=4), "0"),
                     ("host T=8", dict(cpu_max=-1, threads=8), "0"),
-                    ("split T=8 (hostfast)", dict(threads=8, split=True), "1"),
+                    ("default T=8 (split)", dict(threads=8), "0"),
                     ("host T=16", dict(cpu_max=-1, threads=16), "0"),
-                    ("split T=16 (hostfast)", dict(threads=16, split=True), "1")]
+                    ("default T=16 (split)", dict(threads=16), "0")]
         res = {name: [] for name, _, _ in settings}
         ref = None
         for r in range(rounds):
             order = settings if r % 2 == 0 else settings[::-1]
             for name, kw, hf in order:
-                os.environ["CIOA_SPLIT_HOSTFAST"] = hf
                 cio.route(reset=True, **kw)
                 out = cf.verify_paths(paths)
                 ts = []
@@ -69,7 +67,7 @@ def main():
                 res[name].append(region / min(ts) / 1e9)
             print(f"round {r}: " + "  ".join(f"{n} {res[n][-1]:.1f}" for n, _, _ in settings), flush=True)
         cio.route(reset=True)
-        os.environ["CIOA_SPLIT_HOSTFAST"] = "0"
+        print("learned split rates (T = 16):", cio.split_rates())
         print("\nGB/s (median of rounds, best of 3 calls each):")
         for n, _, _ in settings:
             print(f"  {n:24s} {np.median(res[n]):7.1f}   [{min(res[n]):.1f} .. {max(res[n]):.1f}]")
