@@ -206,10 +206,18 @@ static int route_to_cpu(const size_t *lens, size_t n, const int *devices, int nd
  * bytes and is predicted to finish before the better engine alone; this
  * covers batches the threshold sends to the GPU (one host thread: the caller
  * joins in) and batches it keeps on the host (T threads outrun one PCIe link,
- * and the GPU adds its share).  Results are the same as either engine alone.
- * Measured on the 1000 perf files (profiles/r05/split_probe_*.txt). */
+ * and the GPU adds its share while the host is less than kMaxHostOverGpu
+ * times faster).  Results are the same as either engine alone.  Measured on
+ * the 1000 perf files (profiles/r05/split_probe_r05j*.txt). */
 static const double kCpuThreadFdGBps = 22.0;
 static const double kMinGpuShare = 32e6;
+/* A host-routed batch is shared only while the host's (learned, concurrent)
+ * rate is below this multiple of the GPUs': the GPU path's copy and pread
+ * threads slow the host CRC threads, which pays while the GPU adds a large
+ * share and not once the host is far faster.  Verify of the 1000 perf files
+ * (profiles/r05/split_probe_r05j*.txt): host/GPU 0.35 (1 thread) +32%, 1.2
+ * (4) +40%, 2.3 (8) +9-15%, 3.6-3.9 (16) -5-7%. */
+static const double kMaxHostOverGpu = 3.0;
 enum { kMaxT = 64 };
 static double g_rh[2][kMaxT + 1];        /* learned host rate in a split, GB/s (0: none yet) */
 static double g_rg[2];                   /* learned GPU rate per device in a split, GB/s */
@@ -322,6 +330,9 @@ static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int f
     double total = 0;
     for (size_t i = 0; i < n; i++) {
         total += (double) lens[i];
+    }
+    if (mode != 2 && !gpu_bound && r_host >= kMaxHostOverGpu * r_gpu) {
+        return 0;     /* the host alone (see kMaxHostOverGpu) */
     }
     const double b_host = (f + total / r_gpu) / (1.0 / r_host + 1.0 / r_gpu);
     const double t_split = b_host / r_host;
