@@ -1208,8 +1208,10 @@ def run_verify(args, rank, world, device, dist, compact=False):
             # `value` is the default route: GPU-bound batches split with the
             # calling thread (crc_route.c); gpu_alone is the same call with
             # the split route off (every CRC byte on the GPU).
+            nt = host_cpu_threads()
             for tag, kw in (("gpu_alone", {"split": False}), ("threads_1", {"cpu_max": -1, "threads": 1}),
-                            (f"threads_{host_cpu_threads()}", {"threads": host_cpu_threads()})):
+                            (f"threads_{nt}", {"cpu_max": -1, "threads": nt}),
+                            (f"default_route_threads_{nt}", {"threads": nt})):
                 cio.route(reset=True, **kw)
                 cf.verify_paths(paths)
                 ht = []
@@ -1225,7 +1227,9 @@ def run_verify(args, rank, world, device, dist, compact=False):
             cio.route(reset=True)
         host_route["note"] = ("cio_verify_paths with the CRC batch routed to the library's host crc_update "
                               "(cio_crc32_batch_fd_cpu: pread + VPCLMULQDQ folding) instead of the GPU; "
-                              "gpu_alone: the GPU without the split route's host share")
+                              "gpu_alone: the GPU without the split route's host share; default_route_threads_N: "
+                              "the default route with N host threads (the split route shares the batch with "
+                              "the GPU while the host is < 3x faster than it)")
         cpu = None
         if rank == 0 and not args.no_cpu:
             import mmap
