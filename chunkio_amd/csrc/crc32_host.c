@@ -192,12 +192,14 @@ static uint32_t crc_vclmul(uint32_t c, const unsigned char *p, size_t len)
 /* CIOA_HOST_CRC=table forces the table path (A/B and tests). */
 static int host_crc_mode(void)
 {
-    static int mode = -1;
-    if (mode < 0) {
+    static int mode = -1;     /* read once; concurrent first callers compute the same value */
+    int m = __atomic_load_n(&mode, __ATOMIC_RELAXED);
+    if (m < 0) {
         const char *r = getenv("CIOA_HOST_CRC");
-        mode = (r && strcmp(r, "table") == 0) ? 0 : (r && strcmp(r, "clmul") == 0) ? 1 : 2;
+        m = (r && strcmp(r, "table") == 0) ? 0 : (r && strcmp(r, "clmul") == 0) ? 1 : 2;
+        __atomic_store_n(&mode, m, __ATOMIC_RELAXED);
     }
-    return mode;
+    return m;
 }
 
 uint64_t cioa_crc_update_host(uint64_t crc, const void *data, size_t len)

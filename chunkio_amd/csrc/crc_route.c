@@ -228,8 +228,8 @@ int cio_crc32_split_route(void)
     if (v >= 0) {
         return v;
     }
-    const char *r = getenv("CIOA_SPLIT_ROUTE");
-    return !(r && strcmp(r, "0") == 0);
+    const char *r = getenv("CIOA_SPLIT_ROUTE");     /* "0" off, "2" forced (tests), else on */
+    return r && strcmp(r, "0") == 0 ? 0 : r && strcmp(r, "2") == 0 ? 2 : 1;
 }
 
 void cio_crc32_set_split_route(int on)

@@ -264,7 +264,7 @@ void   cio_crc32_set_cpu_max(size_t bytes);
  * explicit threshold (cio_crc32_set_cpu_max / CIOA_CPU_CRC_MAX) picks one
  * engine unless set_split_route(1) was also called; 0 is always the GPU
  * alone.  set_split_route(2) forces a split of every batch of 2+ chunks
- * (tests).  split_rates: {host memory T=1, host file T=1, host memory T,
+ * (tests; also CIOA_SPLIT_ROUTE=2).  split_rates: {host memory T=1, host file T=1, host memory T,
  * host file T, GPU memory, GPU file} GB/s the next split is sized with, T =
  * cio_crc32_host_threads(); split_forget drops what was learned. */
 int    cio_crc32_split_route(void);

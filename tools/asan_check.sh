@@ -69,11 +69,12 @@ host|gpu)
         # still quarantined when libamdhip64's destructors unload the runtime
         # trips its "device runtime unloaded" CHECK at exit (seen in r04ao).
         export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:quarantine_size_mb=0
-        # CIOA_CPU_CRC_MAX=0: every batch on the GPU alone; =1: every batch of
-        # two or more chunks on the split route (GPU helper thread + host)
+        # CIOA_CPU_CRC_MAX=0: every batch on the GPU alone; =1 with
+        # CIOA_SPLIT_ROUTE=2: every batch of two or more chunks on the split
+        # route (GPU helper thread + host, learned rates)
         for cm in 0 1; do
             for m in immediate deferred; do
-                CIOA_CPU_CRC_MAX=$cm timeout -k 10 300 $BIN/test_chunk_api $DATA "$W" $m
+                CIOA_CPU_CRC_MAX=$cm CIOA_SPLIT_ROUTE=$((cm * 2)) timeout -k 10 300 $BIN/test_chunk_api $DATA "$W" $m
             done
         done
         timeout -k 10 300 $BIN/test_multi "$W"
@@ -114,7 +115,7 @@ tsan|tsan-gpu)
         else
             for cm in 0 1; do
                 TSAN_OPTIONS=halt_on_error=1:suppressions=$PWD/tools/tsan_rocm.supp CIOA_CPU_CRC_MAX=$cm \
-                    timeout -k 10 300 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m
+                    CIOA_SPLIT_ROUTE=$((cm * 2)) timeout -k 10 300 $TB/test_chunk_api tests/golden/400kb.txt "$W" $m
             done
         fi
     done

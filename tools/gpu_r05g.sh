@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 GPU session g: sanitizers on the GPU route, now also the split route.
 set -u
-O=gpurun_out/r05g
+O=gpurun_out/${1:-r05g}
 mkdir -p $O
 export TMPDIR=/tmp
 step() { local rc=$1 what=$2; echo "[$what] rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stop after $what"; exit "$rc"; fi; }
