@@ -348,6 +348,13 @@ static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int f
     return k;
 }
 
+/* Test hook (not in the public header; no device needed for a batch the
+ * threshold sends to the GPU): the split point split_point() picks. */
+size_t cioa_debug_split_point(const size_t *lens, size_t n, int ndev_distinct, int fd, int gpu_bound)
+{
+    return split_point(lens, n, ndev_distinct, fd, gpu_bound);
+}
+
 struct gpu_part {
     const void *const *bufs;
     const int *fds;

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import chunkio_amd as cio
+from chunkio_amd import _lib
 from chunkio_amd import workloads as wl
 from oracle import pyoracle as po
 
@@ -163,3 +164,45 @@ def test_route_threshold_follows_host_threads():
             cio.route(cpu_max=before_max)
         if before_t != 1:
             cio.route(threads=before_t)
+
+
+def test_split_point_sizing_model():
+    """crc_route.c's split sizing for a batch the threshold sends to the GPU
+    (no device needed): the host takes the largest suffix of whole chunks
+    within B_host = (F + B / r_gpu) / (1 / r_host + 1 / r_gpu) at the model's
+    rates; nothing is split when the GPU's share would be under 32 MB, when the
+    split route is off, or when an explicit threshold picks the engine."""
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.cioa_debug_split_point
+    f.restype = ctypes.c_size_t
+    f.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    if os.environ.get("CIOA_CPU_CRC_MAX") or os.environ.get("CIOA_SPLIT_ROUTE") or os.environ.get("CIOA_HOST_CRC_THREADS"):
+        pytest.skip("routing environment set by the caller")
+
+    def point(lens, fd=1, ndev=1):
+        arr = (ctypes.c_size_t * len(lens))(*lens)
+        return int(f(arr, len(lens), ndev, fd, 1))
+
+    try:
+        cio.route(reset=True, threads=1)
+        cio.split_rates(forget=True)
+        lens = [2048002] * 1000                            # the verify leg's 1000 perf files
+        B = float(sum(lens))
+        for fd, r_host in ((1, 22.0), (0, 36.0)):
+            for ndev in (1, 2):
+                r_gpu = 54.7 * ndev
+                b_host = (163.5e-6 + B / (r_gpu * 1e9)) / (1 / (r_host * 1e9) + 1 / (r_gpu * 1e9))
+                k = point(lens, fd, ndev)
+                assert sum(lens[k:]) <= b_host < sum(lens[k - 1:]), (fd, ndev, k)
+        assert point([2048002] * 12) == 12                 # 24.6 MB: the GPU's share would be < 32 MB
+        cio.route(split=False)
+        assert point(lens) == len(lens)
+        cio.route(reset=True, cpu_max=1)                   # explicit threshold: the GPU alone
+        assert point(lens) == len(lens)
+        cio.route(split=True)                              # ... unless the split is turned on too
+        assert point(lens) < len(lens)
+        cio.route(reset=True, cpu_max=1, split="force")    # forced: even 2 chunks of 1 byte
+        assert point([1, 1]) == 1
+    finally:
+        cio.route(reset=True)
+        cio.split_rates(forget=True)
