@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <crc32/crc32.h>
@@ -134,6 +135,7 @@ static uint64_t g_gen;                /* batch generation */
 static struct cpu_job *g_job;
 static int g_want;                    /* workers taking part in this batch */
 static int g_pending;
+static int g_stop;                    /* library unload / process exit: workers leave */
 
 struct worker_arg {
     int idx;
@@ -148,8 +150,14 @@ static void *worker(void *arg)
     uint64_t seen = wa.seen;    /* so a worker started for this batch joins it */
     pthread_mutex_lock(&g_mu);
     for (;;) {
-        while (g_gen == seen) {
+        while (g_gen == seen && !g_stop) {
             pthread_cond_wait(&g_cv, &g_mu);
+        }
+        if (g_stop) {
+            g_started--;
+            pthread_cond_broadcast(&g_done_cv);
+            pthread_mutex_unlock(&g_mu);
+            return NULL;
         }
         seen = g_gen;
         if (idx >= g_want) {
@@ -166,11 +174,34 @@ static void *worker(void *arg)
     return NULL;
 }
 
+/* The pool's detached workers run this library's code: on dlclose (or at
+ * exit) they are told to leave and waited for, at most 2 s, so none is left
+ * executing unmapped code.  A worker in the middle of a batch finishes its
+ * tasks first. */
+__attribute__((destructor)) static void pool_stop(void)
+{
+    pthread_mutex_lock(&g_mu);
+    g_stop = 1;
+    pthread_cond_broadcast(&g_cv);
+    struct timespec dl;
+    clock_gettime(CLOCK_REALTIME, &dl);
+    dl.tv_sec += 2;
+    while (g_started > 0) {
+        if (pthread_cond_timedwait(&g_done_cv, &g_mu, &dl) != 0) {
+            break;
+        }
+    }
+    pthread_mutex_unlock(&g_mu);
+}
+
 /* Runs j on the caller plus up to helpers pool workers; returns after all
  * of them are done with it. */
 static void pool_run(struct cpu_job *j, int helpers)
 {
     pthread_mutex_lock(&g_mu);
+    if (g_stop) {
+        helpers = 0;          /* (a batch during unload: the caller alone) */
+    }
     while (g_started < helpers) {
         pthread_t th;
         pthread_attr_t at;

@@ -206,3 +206,28 @@ def test_split_point_sizing_model():
     finally:
         cio.route(reset=True)
         cio.split_rates(forget=True)
+
+
+def test_library_unload_stops_the_host_crc_pool():
+    """The host CRC pool's detached workers run the library's code: dlclose
+    (and exit) tells them to leave first (crc_cpu_batch.c pool_stop), so a
+    process that unloads the library after an 8-thread batch keeps running."""
+    import subprocess
+    import sys
+    code = f"""
+import ctypes, _ctypes, time, numpy as np
+lib = ctypes.CDLL({_lib.LIB_PATH!r}, mode=ctypes.RTLD_LOCAL)
+n = 64
+bufs = [np.full(1 << 20, i, np.uint8) for i in range(n)]
+ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+lens = (ctypes.c_size_t * n)(*[b.size for b in bufs])
+out = (ctypes.c_uint32 * n)()
+assert lib.cio_crc32_batch_cpu(ptrs, lens, None, out, n, 8) == 0
+h = lib._handle
+del lib
+_ctypes.dlclose(h)
+time.sleep(0.5)
+print("alive")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "alive", (r.returncode, r.stderr[-2000:])
