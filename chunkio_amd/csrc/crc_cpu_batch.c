@@ -136,6 +136,7 @@ static struct cpu_job *g_job;
 static int g_want;                    /* workers taking part in this batch */
 static int g_pending;
 static int g_stop;                    /* library unload / process exit: workers leave */
+static pthread_t g_tid[kMaxThreads];  /* joinable, so unload can wait for them */
 
 struct worker_arg {
     int idx;
@@ -154,8 +155,6 @@ static void *worker(void *arg)
             pthread_cond_wait(&g_cv, &g_mu);
         }
         if (g_stop) {
-            g_started--;
-            pthread_cond_broadcast(&g_done_cv);
             pthread_mutex_unlock(&g_mu);
             return NULL;
         }
@@ -182,16 +181,18 @@ __attribute__((destructor)) static void pool_stop(void)
 {
     pthread_mutex_lock(&g_mu);
     g_stop = 1;
+    const int n = g_started;
     pthread_cond_broadcast(&g_cv);
+    pthread_mutex_unlock(&g_mu);
     struct timespec dl;
     clock_gettime(CLOCK_REALTIME, &dl);
     dl.tv_sec += 2;
-    while (g_started > 0) {
-        if (pthread_cond_timedwait(&g_done_cv, &g_mu, &dl) != 0) {
+    for (int i = 0; i < n; i++) {
+        /* joined, not counted: a worker is only gone once it has returned */
+        if (pthread_timedjoin_np(g_tid[i], NULL, &dl) != 0) {
             break;
         }
     }
-    pthread_mutex_unlock(&g_mu);
 }
 
 /* Runs j on the caller plus up to helpers pool workers; returns after all
@@ -212,14 +213,13 @@ static void pool_run(struct cpu_job *j, int helpers)
         wa->idx = g_started;
         wa->seen = g_gen;
         pthread_attr_init(&at);
-        pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
-        const int ok = pthread_create(&th, &at, worker, wa) == 0;
+        const int ok = g_started < kMaxThreads && pthread_create(&th, &at, worker, wa) == 0;
         pthread_attr_destroy(&at);
         if (!ok) {
             free(wa);
             break;
         }
-        g_started++;
+        g_tid[g_started++] = th;
     }
     if (helpers > g_started) {
         helpers = g_started;
