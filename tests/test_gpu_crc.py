@@ -964,3 +964,22 @@ def test_verify_paths_large_files_across_staging_groups(cuda, tmp_path):
     assert int(st[0]) == cf.CIO_CORRUPTED and int(er[0]) == cf.CIO_ERR_BAD_CHECKSUM
     assert list(st[1:]) == [cf.CIO_OK] * (len(paths) - 1)
     assert [int(r) ^ 0xFFFFFFFF for r in raw[1:]] == crcs[1:]
+
+
+def test_pci_bus_id_names_the_device(cuda):
+    """cio_gpu_pci_bus_id: the PCI address of an ordinal, as the bench's
+    topology records it ("dddd:bb:dd.f"); agrees with torch's device
+    properties; a short buffer is refused with a message."""
+    import ctypes
+    import re
+    import torch
+    lib = cio.lib()
+    buf = ctypes.create_string_buffer(64)
+    assert lib.cio_gpu_pci_bus_id(0, buf, 64) == 0
+    bus = buf.value.decode()
+    assert re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-9a-f]", bus.lower()), bus
+    p = torch.cuda.get_device_properties(0)
+    if hasattr(p, "pci_bus_id"):
+        assert int(bus.split(":")[1], 16) == int(p.pci_bus_id), (bus, p.pci_bus_id)
+    assert lib.cio_gpu_pci_bus_id(0, buf, 8) != 0
+    assert b"13 bytes" in lib.cio_gpu_last_error()
