@@ -61,7 +61,10 @@ def main():
     dev = torch.device("cuda:0")
     results = {}
     for cfg in args.cfg.split(","):
+        if cfg.startswith("k4x"):       # k4x<n>: n chunks of 4 KiB
+            k4n = int(cfg[3:])
         lens = {"cfg2": wl.cfg2_lens, "cfg3": wl.cfg3_lens,
+                cfg: lambda: np.full(k4n, 4096, np.uint64),
                 "big": lambda: np.full(1024, 4 << 20, np.uint64),
                 "cfg4": lambda: np.full(8192, 4 << 20, np.uint64),
                 "mid": lambda: np.full(1024, 1638400, np.uint64),
