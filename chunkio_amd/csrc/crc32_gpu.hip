@@ -2184,6 +2184,28 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
             ph = std::move(ph4);
         }
     }
+    // HBM channel camping (profiles/r05/camping/): when every wave's range is
+    // the same multiple of 16 steps (64 KiB), all waves read addresses equal
+    // modulo 64 KiB at the same moment and even the read-only stream loses
+    // 5-10 % (16, 32, 48, 64 steps per wave against 17, 33, 50, 65).  One
+    // workgroup fewer per 32 -- one per XCD, so the XCDs stay balanced --
+    // makes the ranges uneven and breaks the congruence.  CIO_GPU_ANTICAMP=0
+    // keeps the full grid (A/B).
+    {
+        const char *r = getenv("CIO_GPU_ANTICAMP");
+        const bool on = !(r && atoi(r) == 0);
+        const uint64_t w = p->W ? ph.S / p->W : 0;
+        if (on && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 && w % 16 == 0 && w > 0 &&
+            w <= 64) {
+            const uint32_t g2 = p->grid / 32 * 31;
+            PlanHost ph2;
+            if (plan_build(ph2, offs, lens, n, g2 * (kThreads / kWave)) == nullptr) {
+                p->grid = g2;
+                p->W = g2 * (kThreads / kWave);
+                ph = std::move(ph2);
+            }
+        }
+    }
     p->S = ph.S;
     p->bytes = ph.bytes;
     p->ntiny = (uint32_t) ph.tiny.size();
