@@ -2175,12 +2175,14 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // out the per-CU finish times (cfg3 -0.7 %, cfg4 -1.7 %; shorter ranges
     // lose: 1 MiB per wave +0.8 to +5.5 %, cfg2 +5 %:
     // profiles/r04/ab_grid_oversubscribed_r04q.txt, ab_grid_cfg4_r04x.txt).
+    bool oversub = false;
     if (!getenv("CIO_GPU_GRID") && ph.S >= 1024ull * p->W && 4ull * p->W <= 65536 &&
         ph.S != (uint64_t) n - ph.tiny.size()) {    // (not a small-chunk batch)
         PlanHost ph4;
         if (plan_build(ph4, offs, lens, n, 4 * p->W) == nullptr) {
             p->grid *= 4;
             p->W *= 4;
+            oversub = true;
             ph = std::move(ph4);
         }
     }
@@ -2194,9 +2196,11 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     {
         const char *r = getenv("CIO_GPU_ANTICAMP");
         const bool on = !(r && atoi(r) == 0);
+        const char *mx = getenv("CIO_GPU_ANTICAMP_MAX");     // A/B: longest range it applies to
+        const uint64_t wmax = mx ? strtoull(mx, nullptr, 10) : 64;
         const uint64_t w = p->W ? ph.S / p->W : 0;
-        if (on && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 && w % 16 == 0 && w > 0 &&
-            w <= 64) {
+        if (on && !oversub && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 && w % 16 == 0 &&
+            w > 0 && w <= wmax) {
             const uint32_t g2 = p->grid / 32 * 31;
             PlanHost ph2;
             if (plan_build(ph2, offs, lens, n, g2 * (kThreads / kWave)) == nullptr) {

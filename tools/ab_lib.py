@@ -61,10 +61,13 @@ def main():
     dev = torch.device("cuda:0")
     results = {}
     for cfg in args.cfg.split(","):
+        k4n, klen = 0, 4096
         if cfg.startswith("k4x"):       # k4x<n>: n chunks of 4 KiB
             k4n = int(cfg[3:])
+        elif cfg.startswith("c") and "kx" in cfg:   # c<K>kx<n>: n chunks of K KiB
+            klen, k4n = int(cfg[1:cfg.index("kx")]) << 10, int(cfg[cfg.index("kx") + 2:])
         lens = {"cfg2": wl.cfg2_lens, "cfg3": wl.cfg3_lens,
-                cfg: lambda: np.full(k4n, 4096, np.uint64),
+                cfg: lambda: np.full(k4n, klen, np.uint64),
                 "big": lambda: np.full(1024, 4 << 20, np.uint64),
                 "cfg4": lambda: np.full(8192, 4 << 20, np.uint64),
                 "mid": lambda: np.full(1024, 1638400, np.uint64),
