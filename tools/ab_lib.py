@@ -11,6 +11,7 @@ identical; rounds interleave the libraries so clock/thermal drift hits both.
 import argparse
 import ctypes
 import json
+import time
 import os
 import sys
 
@@ -43,6 +44,7 @@ def main():
     ap.add_argument("--cfg", default="cfg2,big")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--warm-s", type=float, default=1.0, help="untimed launches before each batch's rounds")
     ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the output equality check")
     args = ap.parse_args()
     import torch
@@ -110,8 +112,18 @@ def main():
             assert args.no_check or np.array_equal(got, ref), f"{cfg}: outputs differ"
         times = [[] for _ in libs]
         times_b2b = [[] for _ in libs]
+        # Warm the clocks first: short A/Bs on a cold GPU drift faster round
+        # by round (profiles/r05/camping/), which biases the later libs.
+        t_end = time.perf_counter() + args.warm_s
+        while time.perf_counter() < t_end:
+            for k in range(8):
+                libs[0].cio_crc32_plan_exec(plans[0], bufs[k % nrot].data_ptr(), None, outs[0].data_ptr(), stream)
+            torch.cuda.synchronize()
+        order = list(range(len(libs)))
         for r in range(args.rounds):
-            for i, (lib, p, o) in enumerate(zip(libs, plans, outs)):
+            # ABBA: odd rounds run the libs in reverse order
+            for i in (order if r % 2 == 0 else order[::-1]):
+                lib, p, o = libs[i], plans[i], outs[i]
                 evs = [(lib.cio_gpu_event_create(), lib.cio_gpu_event_create()) for _ in range(args.iters)]
                 for k in range(3):
                     lib.cio_crc32_plan_exec(p, bufs[k % nrot].data_ptr(), None, o.data_ptr(), stream)
