@@ -33,6 +33,7 @@ def load(path):
     lib.cio_gpu_event_elapsed_ms.restype = ctypes.c_float
     lib.cio_gpu_event_elapsed_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.cio_gpu_event_record.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.cio_gpu_event_destroy.argtypes = [ctypes.c_void_p]
     lib.cio_gpu_version.restype = ctypes.c_char_p
     return lib
 
@@ -120,20 +121,27 @@ def main():
                 libs[0].cio_crc32_plan_exec(plans[0], bufs[k % nrot].data_ptr(), None, outs[0].data_ptr(), stream)
             torch.cuda.synchronize()
         order = list(range(len(libs)))
+        # one set of events per lib for the whole batch, destroyed after it
+        all_evs = [[(lib.cio_gpu_event_create(), lib.cio_gpu_event_create()) for _ in range(args.iters)]
+                   for lib in libs]
+        all_b2b = [(lib.cio_gpu_event_create(), lib.cio_gpu_event_create()) for lib in libs]
+        assert all(e for evs in all_evs for pair in evs for e in pair) and all(e for pr in all_b2b for e in pr)
         for r in range(args.rounds):
             # ABBA: odd rounds run the libs in reverse order
             for i in (order if r % 2 == 0 else order[::-1]):
                 lib, p, o = libs[i], plans[i], outs[i]
-                evs = [(lib.cio_gpu_event_create(), lib.cio_gpu_event_create()) for _ in range(args.iters)]
+                evs = all_evs[i]
                 for k in range(3):
                     lib.cio_crc32_plan_exec(p, bufs[k % nrot].data_ptr(), None, o.data_ptr(), stream)
                 for k in range(args.iters):
                     lib.cio_crc32_plan_exec_events(p, bufs[k % nrot].data_ptr(), None, o.data_ptr(),
                                                    stream, evs[k][0], evs[k][1])
                 torch.cuda.synchronize()
-                us = float(np.mean([lib.cio_gpu_event_elapsed_ms(a, b) for a, b in evs])) * 1e3
+                ms = [lib.cio_gpu_event_elapsed_ms(a, b) for a, b in evs]
+                assert min(ms) > 0, f"{cfg}: event timing failed"
+                us = float(np.mean(ms)) * 1e3
                 # back-to-back launches under one event pair (no per-launch events)
-                b0, b1 = lib.cio_gpu_event_create(), lib.cio_gpu_event_create()
+                b0, b1 = all_b2b[i]
                 lib.cio_gpu_event_record(b0, stream)
                 for k in range(args.iters):
                     lib.cio_crc32_plan_exec(p, bufs[k % nrot].data_ptr(), None, o.data_ptr(), stream)
@@ -148,8 +156,10 @@ def main():
             med = float(np.median(times[i]))
             results[f"{cfg}/lib{i}"] = {"us": round(med, 2), "GBps": round(total / med / 1e3, 1),
                                         "b2b_us": round(float(np.median(times_b2b[i])), 2)}
-        for lib, p in zip(libs, plans):
+        for lib, p, evs, pr in zip(libs, plans, all_evs, all_b2b):
             lib.cio_crc32_plan_destroy(p)
+            for e in [x for pair in evs for x in pair] + list(pr):
+                lib.cio_gpu_event_destroy(e)
         del bufs
         torch.cuda.empty_cache()
     print(json.dumps(results))
