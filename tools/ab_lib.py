@@ -69,13 +69,15 @@ def main():
             k4n = int(cfg[3:])
         elif cfg.startswith("c") and "kx" in cfg:   # c<K>kx<n>: n chunks of K KiB
             klen, k4n = int(cfg[1:cfg.index("kx")]) << 10, int(cfg[cfg.index("kx") + 2:])
-        lens = {"cfg2": wl.cfg2_lens, "cfg3": wl.cfg3_lens,
-                cfg: lambda: np.full(k4n, klen, np.uint64),
+        lens = (lambda: np.full(k4n, klen, np.uint64)) if k4n else {
+                "cfg2": wl.cfg2_lens, "cfg3": wl.cfg3_lens,
                 "big": lambda: np.full(1024, 4 << 20, np.uint64),
                 "cfg4": lambda: np.full(8192, 4 << 20, np.uint64),
                 "mid": lambda: np.full(1024, 1638400, np.uint64),
                 "small": lambda: np.full(65536, 4096, np.uint64),
-                "cfg4k": lambda: np.full(102400, 4096, np.uint64)}[cfg]()
+                "cfg4k": lambda: np.full(102400, 4096, np.uint64)}[cfg]
+        lens = lens()
+        assert len(lens) > 0, cfg
         lens = np.ascontiguousarray(lens, dtype=np.uint64)
         offs = np.ascontiguousarray(wl.packed_offsets(lens, align=16), dtype=np.uint64)
         total = int(wl.batch_bytes(offs, lens))
