@@ -2189,15 +2189,19 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // HBM channel camping (profiles/r05/camping/): when every wave's range is
     // the same multiple of 16 steps (64 KiB), all waves read addresses equal
     // modulo 64 KiB at the same moment and even the read-only stream loses
-    // 5-10 % (16, 32, 48, 64 steps per wave against 17, 33, 50, 65).  One
-    // workgroup fewer per 32 -- one per XCD, so the XCDs stay balanced --
-    // makes the ranges uneven and breaks the congruence.  CIO_GPU_ANTICAMP=0
-    // keeps the full grid (A/B).
+    // 5-10 % (16, 32, 64 steps per wave against 17, 33, 65).  One workgroup
+    // fewer per 32 -- one per XCD, so the XCDs stay balanced -- makes the
+    // ranges uneven and breaks the congruence.  Warm ABBA A/B
+    // (ab_anticamp_abba_r05x.txt): stream kernel +4.1 to +4.6 % at 16-64
+    // steps per wave, -1.0 % at 128 and 256; small-chunk kernel +10.9 to
+    // +14.3 % at 16-64 chunks per wave, +3.3 % at 128.  CIO_GPU_ANTICAMP=0
+    // keeps the full grid; CIO_GPU_ANTICAMP_MAX overrides the range cap.
     {
         const char *r = getenv("CIO_GPU_ANTICAMP");
         const bool on = !(r && atoi(r) == 0);
         const char *mx = getenv("CIO_GPU_ANTICAMP_MAX");     // A/B: longest range it applies to
-        const uint64_t wmax = mx ? strtoull(mx, nullptr, 10) : 64;
+        const bool small_batch = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
+        const uint64_t wmax = mx ? strtoull(mx, nullptr, 10) : small_batch ? 128 : 64;
         const uint64_t w = p->W ? ph.S / p->W : 0;
         if (on && !oversub && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 && w % 16 == 0 &&
             w > 0 && w <= wmax) {

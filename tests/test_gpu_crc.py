@@ -440,6 +440,42 @@ def test_plan_workgroups(cuda, monkeypatch):
         assert p3.workgroups == 17
 
 
+@pytest.mark.parametrize("clen,per_wave,reduced", [(4096, 16, True), (4096, 128, True), (4096, 25, False),
+                                                   (4096, 256, False), (65536, 16, True), (65536, 64, True),
+                                                   (65536, 25, False), (65536, 128, False)])
+def test_anticamp_grid(cuda, monkeypatch, clen, per_wave, reduced):
+    """Batches whose even split gives every wave the same multiple of 16 steps
+    (small-chunk batches up to 128 chunks per wave, stream batches up to 64
+    steps) plan one workgroup fewer per XCD (31 of every 32); the CRCs are the
+    oracle's on both grids (CIO_GPU_ANTICAMP=0 keeps the full one)."""
+    import torch
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    if cus % 32:
+        pytest.skip("grid not a multiple of 32 workgroups")
+    steps = clen // 4096
+    n = cus * 16 * per_wave // steps
+    lens = np.full(n, clen, np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    dev = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, 0xCA4F + per_wave)
+    host = dev.cpu().numpy()
+    want = po.crc_batch(host, offs, lens) if n * clen <= (64 << 20) else None
+    got = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("CIO_GPU_ANTICAMP", env)
+        with cio.Crc32Plan(offs, lens) as p:
+            assert p.workgroups == (cus // 32 * 31 if reduced and env == "1" else cus), env
+            out = torch.empty(n, dtype=torch.int32, device=cuda)
+            p.exec(dev, out)
+            got[env] = out.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got["1"], got["0"])
+    if want is not None:
+        np.testing.assert_array_equal(got["1"], want)
+    else:
+        idx = np.arange(0, n, 997)
+        np.testing.assert_array_equal(got["1"][idx], po.crc_batch(host, offs[idx], lens[idx]))
+
+
 def test_read_stream_grids(cuda):
     """The read-only ceiling kernel (bench.py's roofline.read_stream) on one
     and four workgroups per CU and on a small grid; more than 4096
