@@ -2194,7 +2194,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // ranges uneven and breaks the congruence.  Warm ABBA A/B
     // (ab_anticamp_abba_r05x.txt): stream kernel +4.1 to +4.6 % at 16-64
     // steps per wave, -1.0 % at 128 and 256; small-chunk kernel +10.9 to
-    // +14.3 % at 16-64 chunks per wave, +3.3 % at 128.  CIO_GPU_ANTICAMP=0
+    // +14.3 % at 16-64 chunks per wave, +3.9 % at 128.  CIO_GPU_ANTICAMP=0
     // keeps the full grid; CIO_GPU_ANTICAMP_MAX overrides the range cap.
     {
         const char *r = getenv("CIO_GPU_ANTICAMP");
