@@ -346,6 +346,29 @@ def test_one_huge_chunk_spans_all_waves(cuda):
         assert int(got[0]) == po.crc_update(seed, data)
 
 
+def test_chunk_longer_than_4gib(cuda):
+    """One chunk of 4 GiB + 4097 bytes (length and offsets past 32 bits),
+    misaligned, between two small chunks, with and without a seed: zlib's
+    CRC of the same bytes (the reference's crc_update takes a size_t length,
+    crc32.c:337)."""
+    import zlib
+    import torch
+    n = (4 << 30) + 4097
+    lens = np.asarray([1000, n, 777], np.uint64)
+    offs = np.asarray([3, 1024 + 5, 1024 + 5 + n + 11], np.uint64)
+    dev = torch.empty(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, 0x4C16)
+    host = dev.cpu().numpy()
+    want = [zlib.crc32(memoryview(host[int(o):int(o + ln)])) ^ INIT for o, ln in zip(offs, lens)]
+    got = cio.crc32_batch_dev(dev, offs, lens)
+    assert [int(x) for x in got] == want
+    seeds = np.asarray([0x12345678, 0x9ABCDEF0, 0], np.uint32)
+    got = cio.crc32_batch_dev(dev, offs, lens, seeds=seeds)
+    want = [zlib.crc32(memoryview(host[int(o):int(o + ln)]), int(s) ^ INIT) ^ INIT
+            for o, ln, s in zip(offs, lens, seeds)]
+    assert [int(x) for x in got] == want
+
+
 def test_plan_reuse_on_stream(cuda):
     import torch
     lens = wl.cfg2_lens(64)
