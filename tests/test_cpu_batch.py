@@ -231,3 +231,22 @@ print("alive")
 """
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "alive", (r.returncode, r.stderr[-2000:])
+
+
+def test_host_paths_past_4gib():
+    """Host CRC over 4 GiB + 5 bytes (lengths and offsets past 32 bits): the
+    drop-in crc_update (crc32.c:337 takes a size_t length) and the host batch
+    pool on 1 and 4 threads, against zlib.  The data repeats every 1,000,003
+    bytes, so a 32-bit offset wrap would read different bytes."""
+    import zlib
+    n = (4 << 30) + 5
+    block = np.random.default_rng(44).integers(0, 256, 1_000_003, dtype=np.uint8)
+    buf = np.resize(block, n + 64)
+    want_full = zlib.crc32(memoryview(buf[3:3 + n])) ^ 0xFFFFFFFF
+    assert cio.crc_update(cio.crc_init(), memoryview(buf[3:3 + n])) == want_full
+    offs = np.asarray([0, 3, n + 7], np.uint64)
+    lens = np.asarray([3, n, 50], np.uint64)
+    want = [zlib.crc32(memoryview(buf[int(o):int(o + ln)])) ^ 0xFFFFFFFF for o, ln in zip(offs, lens)]
+    for t in (1, 4):
+        got = cio.crc32_batch_cpu_packed(buf, offs, lens, threads=t)
+        assert [int(x) for x in got] == want, t
