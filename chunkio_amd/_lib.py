@@ -35,14 +35,15 @@ EXPORTS = (
     # include/chunkio_amd/cio_verify.h
     "cio_file_verify_batch", "cio_file_verify_batch_multi", "cio_verify_paths", "cio_verify_paths_multi",
     # include/chunkio_amd/cio_sync.h
-    "cio_file_sync_batch", "cio_file_sync_batch_multi",
+    "cio_file_sync_batch", "cio_file_sync_batch_multi", "cio_file_sync_batch_begin", "cio_file_sync_batch_end",
     # include/chunkio_amd/cioa_chunk.h
     "cioa_create", "cioa_destroy", "cioa_set_max_chunks_up", "cioa_set_realloc_size_hint",
     "cioa_enable_file_trimming", "cioa_disable_file_trimming", "cioa_get_flags", "cioa_set_devices",
     "cioa_last_chunk_error", "cioa_total_chunks", "cioa_total_chunks_up",
     "cioa_stream_create", "cioa_stream_get", "cioa_stream_size_chunks_up", "cioa_stream_chunks", "cioa_scan_stream", "cioa_scan_dump",
     "cioa_chunk_open", "cioa_chunk_close", "cioa_chunk_delete", "cioa_chunk_write", "cioa_chunk_write_at",
-    "cioa_chunk_sync", "cioa_chunk_sync_batch", "cioa_chunk_get_content", "cioa_chunk_get_content_copy",
+    "cioa_chunk_sync", "cioa_chunk_sync_batch", "cioa_chunk_sync_batch_begin", "cioa_chunk_sync_batch_end",
+    "cioa_chunk_get_content", "cioa_chunk_get_content_copy",
     "cioa_chunk_get_content_size", "cioa_chunk_get_real_size", "cioa_chunk_hash", "cioa_chunk_lock",
     "cioa_chunk_unlock", "cioa_chunk_is_locked", "cioa_chunk_tx_begin", "cioa_chunk_tx_commit",
     "cioa_chunk_tx_rollback", "cioa_chunk_is_up", "cioa_chunk_up", "cioa_chunk_up_force", "cioa_chunk_down",

@@ -36,6 +36,7 @@ CIO_OK, CIO_ERROR, CIO_RETRY, CIO_CORRUPTED = 0, -1, -2, -3
 CIO_OPEN, CIO_OPEN_RD, CIO_CHECKSUM, CIO_FULL_SYNC = 1, 2, 4, 8
 CIO_DELETE_IRRECOVERABLE, CIO_TRIM_FILES = 16, 32
 CIOA_DEFERRED_CRC = 128
+CIOA_BENCH_PIPELINED_SYNC = 0x10000      # cioa_bench_perf_write only
 CIO_ERR_BAD_CHECKSUM, CIO_ERR_BAD_LAYOUT, CIO_ERR_PERMISSION, CIO_ERR_BAD_FILE_SIZE = -10, -11, -12, -13
 CIOA_VERIFY_DELETE_IRRECOVERABLE = 16
 CIOA_VERIFY_WRITEBACK = 64
@@ -90,6 +91,10 @@ def _bind():
         "cioa_chunk_write_at": (I, [V, ctypes.c_long, V, S]),
         "cioa_chunk_sync": (I, [V]),
         "cioa_chunk_sync_batch": (I, [ctypes.POINTER(V), S]),
+        "cioa_chunk_sync_batch_begin": (I, [ctypes.POINTER(V), S, ctypes.POINTER(V)]),
+        "cioa_chunk_sync_batch_end": (I, [V]),
+        "cio_file_sync_batch_begin": (I, [ctypes.POINTER(SyncItem), S, I, IP, I, ctypes.POINTER(V)]),
+        "cio_file_sync_batch_end": (I, [V]),
         "cioa_chunk_get_content_size": (ctypes.c_ssize_t, [V]),
         "cioa_chunk_get_real_size": (ctypes.c_ssize_t, [V]),
         "cioa_chunk_hash": (V, [V]),
@@ -373,6 +378,38 @@ def sync_batch(chunks):
     lib = _bind()
     arr = (ctypes.c_void_p * len(chunks))(*[c._c() for c in chunks])
     return int(lib.cioa_chunk_sync_batch(arr, len(chunks)))
+
+
+class SyncJob:
+    """A begun batch sync (cioa_chunk_sync_batch_begin); end() returns what
+    sync_batch would have.  Ended on garbage collection if never ended."""
+
+    def __init__(self, lib, handle):
+        self._lib, self._h = lib, handle
+
+    def end(self):
+        if not self._h:
+            raise ValueError("SyncJob already ended")
+        h, self._h = self._h, None
+        return int(self._lib.cioa_chunk_sync_batch_end(h))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self.end()
+
+
+def sync_batch_begin(chunks):
+    """cioa_chunk_sync_batch_begin: the batch's CRC pass starts on a thread of
+    its own; SyncJob.end() waits for it and writes the headers.  Writing,
+    syncing, a transaction, down or close of one of the chunks ends the batch
+    first."""
+    chunks = [c for c in chunks if c is not None]
+    lib = _bind()
+    arr = (ctypes.c_void_p * max(1, len(chunks)))(*[c._c() for c in chunks])
+    job = ctypes.c_void_p()
+    if lib.cioa_chunk_sync_batch_begin(arr, len(chunks), ctypes.byref(job)) != CIO_OK:
+        raise MemoryError("cioa_chunk_sync_batch_begin")
+    return SyncJob(lib, job.value)
 
 
 class ChunkFile(Chunk):

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <pthread.h>
 #include <arpa/inet.h>
 
 #include <crc32/crc32.h>
@@ -19,30 +20,45 @@
 #include "cio_layout.h"
 #include "crc32_host.h"
 
-int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev)
-{
-    const void **bufs = NULL;
-    size_t *lens = NULL, *idx = NULL, m = 0;
-    uint32_t *seeds = NULL, *raw = NULL;
-    int rc = CIO_OK;
+/* One batch: the ranges (prepare), the routed CRC pass (run, on the calling
+ * thread or on the job's own thread) and the header writes (commit). */
+struct cio_sync_job {
+    cio_sync_item *items;
+    size_t n, m;
+    int flags;
+    const void **bufs;
+    size_t *lens, *idx;
+    uint32_t *seeds, *raw;
+    int devs[64];
+    int ndev;
+    int rc;          /* prepare / run result */
+    int threaded;
+    pthread_t th;
+};
 
-    if (n == 0) {
-        return CIO_OK;
-    }
-    if (!items) {
+static void job_free(cio_sync_job *j)
+{
+    free(j->bufs);
+    free(j->lens);
+    free(j->idx);
+    free(j->seeds);
+    free(j->raw);
+    free(j);
+}
+
+static int job_prepare(cio_sync_job *j)
+{
+    const size_t n = j->n;
+    j->bufs = malloc(n * sizeof(*j->bufs));
+    j->lens = malloc(n * sizeof(*j->lens));
+    j->idx = malloc(n * sizeof(*j->idx));
+    j->seeds = malloc(n * sizeof(*j->seeds));
+    j->raw = malloc(n * sizeof(*j->raw));
+    if (!j->bufs || !j->lens || !j->idx || !j->seeds || !j->raw) {
         return CIO_ERROR;
     }
-    bufs = malloc(n * sizeof(*bufs));
-    lens = malloc(n * sizeof(*lens));
-    idx = malloc(n * sizeof(*idx));
-    seeds = malloc(n * sizeof(*seeds));
-    raw = malloc(n * sizeof(*raw));
-    if (!bufs || !lens || !idx || !seeds || !raw) {
-        rc = CIO_ERROR;
-        goto out;
-    }
     for (size_t i = 0; i < n; i++) {
-        cio_sync_item *it = &items[i];
+        cio_sync_item *it = &j->items[i];
         it->status = CIO_OK;
         if (!it->map || it->fs_size < CIOA_HDR_MIN || it->map[0] != CIOA_HDR_ID_00 ||
             it->map[1] != CIOA_HDR_ID_01) {
@@ -56,46 +72,128 @@ int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags, const i
             it->status = CIO_CORRUPTED;
             continue;
         }
-        bufs[m] = it->map + it->crc_end;
-        lens[m] = (size_t) (end - it->crc_end);
-        seeds[m] = it->crc_cur;
-        idx[m] = i;
-        it->crc_end = end;      /* committed below, after the batch ran */
-        m++;
+        j->bufs[j->m] = it->map + it->crc_end;
+        j->lens[j->m] = (size_t) (end - it->crc_end);
+        j->seeds[j->m] = it->crc_cur;
+        j->idx[j->m] = i;
+        it->crc_end = end;      /* committed in job_commit, after the batch ran */
+        j->m++;
     }
-    if (m > 0 && cioa_crc_batch_route(bufs, lens, seeds, raw, m, devices, ndev) != CIO_OK) {
+    return CIO_OK;
+}
+
+static void *job_run(void *arg)
+{
+    cio_sync_job *j = (cio_sync_job *) arg;
+    j->rc = cioa_crc_batch_route(j->bufs, j->lens, j->seeds, j->raw, j->m, j->ndev > 0 ? j->devs : NULL, j->ndev);
+    return NULL;
+}
+
+static int job_commit(cio_sync_job *j)
+{
+    if (j->rc != CIO_OK) {
         /* restore the ranges: nothing was written */
-        for (size_t k = 0; k < m; k++) {
-            items[idx[k]].crc_end = (uint64_t) ((const unsigned char *) bufs[k] - items[idx[k]].map);
+        for (size_t k = 0; k < j->m; k++) {
+            cio_sync_item *it = &j->items[j->idx[k]];
+            it->crc_end = (uint64_t) ((const unsigned char *) j->bufs[k] - it->map);
         }
-        rc = CIO_ERROR;
-        goto out;
+        return CIO_ERROR;
     }
-    for (size_t k = 0; k < m; k++) {
-        cio_sync_item *it = &items[idx[k]];
-        it->crc_cur = raw[k];
+    for (size_t k = 0; k < j->m; k++) {
+        cio_sync_item *it = &j->items[j->idx[k]];
+        it->crc_cur = j->raw[k];
         crc_t v;
-        if (flags & CIOA_SYNC_FINALIZE) {
-            v = htonl((uint32_t) crc_finalize((crc_t) raw[k]));   /* finalize_checksum */
+        if (j->flags & CIOA_SYNC_FINALIZE) {
+            v = htonl((uint32_t) crc_finalize((crc_t) j->raw[k]));   /* finalize_checksum */
         } else {
-            v = (crc_t) raw[k];                                   /* update_checksum :111 */
+            v = (crc_t) j->raw[k];                                   /* update_checksum :111 */
         }
         memcpy(it->map + 2, &v, sizeof(v));
         /* cio_file_native_sync (src/cio_file_unix.c:477-497): MS_SYNC under
          * CIO_FULL_SYNC, else MS_ASYNC; a failed msync fails the sync
          * (cio_file.c:1231-1236), the chunk stays unsynced. */
-        if ((flags & (CIOA_SYNC_MSYNC | CIOA_SYNC_FULL)) &&
-            msync(it->map, it->fs_size, (flags & CIOA_SYNC_FULL) ? MS_SYNC : MS_ASYNC) != 0) {
+        if ((j->flags & (CIOA_SYNC_MSYNC | CIOA_SYNC_FULL)) &&
+            msync(it->map, it->fs_size, (j->flags & CIOA_SYNC_FULL) ? MS_SYNC : MS_ASYNC) != 0) {
             it->status = CIO_ERROR;
         }
     }
-out:
-    free(bufs);
-    free(lens);
-    free(idx);
-    free(seeds);
-    free(raw);
+    return CIO_OK;
+}
+
+static int job_start(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev, int async,
+                     cio_sync_job **out)
+{
+    *out = NULL;
+    if (n > 0 && !items) {
+        return CIO_ERROR;
+    }
+    cio_sync_job *j = calloc(1, sizeof(*j));
+    if (!j) {
+        return CIO_ERROR;
+    }
+    j->items = items;
+    j->n = n;
+    j->flags = flags;
+    if (n > 0 && (j->rc = job_prepare(j)) != CIO_OK) {
+        job_free(j);
+        return CIO_ERROR;
+    }
+    if (devices && ndev > 0) {
+        j->ndev = ndev < 64 ? ndev : 64;
+        memcpy(j->devs, devices, (size_t) j->ndev * sizeof(int));
+    }
+    else if (async && j->m > 0 && cio_gpu_device_count() > 0) {
+        /* the job's thread runs on the caller's current device */
+        const int cur = cio_gpu_get_device();
+        if (cur >= 0) {
+            j->devs[0] = cur;
+            j->ndev = 1;
+        }
+    }
+    if (j->m > 0) {
+        if (async && pthread_create(&j->th, NULL, job_run, j) == 0) {
+            j->threaded = 1;
+        }
+        else {
+            job_run(j);
+        }
+    }
+    *out = j;
+    return CIO_OK;
+}
+
+int cio_file_sync_batch_begin(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev,
+                              cio_sync_job **job)
+{
+    if (!job) {
+        return CIO_ERROR;
+    }
+    return job_start(items, n, flags, devices, ndev, 1, job);
+}
+
+int cio_file_sync_batch_end(cio_sync_job *job)
+{
+    if (!job) {
+        return CIO_ERROR;
+    }
+    if (job->threaded) {
+        pthread_join(job->th, NULL);
+    }
+    const int rc = job->m > 0 ? job_commit(job) : CIO_OK;
+    job_free(job);
     return rc;
+}
+
+int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    cio_sync_job *j;
+    if (job_start(items, n, flags, devices, ndev, 0, &j) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    return cio_file_sync_batch_end(j);
 }
 
 int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags)

@@ -86,7 +86,10 @@ struct cioa_chunk {
     uint32_t tx_crc;             /* uint32_t as in cio_chunk.h:35 */
     size_t tx_content_length;
     int error_n;
+    struct cioa_sync_job *pending;   /* a begun, not yet ended, batch sync holding this chunk */
 };
+
+static void settle(cioa_chunk *ch);
 
 static int deferred(const cioa_chunk *ch)
 {
@@ -310,6 +313,7 @@ static int full_recompute(cioa_chunk *ch)
  * the raw state at map+2, as update_checksum would have (cio_file.c:111). */
 static int catch_up(cioa_chunk *ch)
 {
+    settle(ch);
     if (!deferred(ch) || !ch->map) {
         return CIO_OK;
     }
@@ -761,6 +765,7 @@ static int munmap_file(cioa_chunk *ch)                       /* cio_file.c:300-3
 
 void cioa_chunk_close(cioa_chunk *ch, int delete_file)
 {
+    settle(ch);
     if (!ch) {
         return;
     }
@@ -805,6 +810,7 @@ int cioa_chunk_is_up(cioa_chunk *ch)
 
 int cioa_chunk_write(cioa_chunk *ch, const void *buf, size_t count)   /* cio_file.c:994-1073 */
 {
+    settle(ch);
     if (count == 0) {
         return 0;
     }
@@ -856,6 +862,7 @@ int cioa_chunk_write(cioa_chunk *ch, const void *buf, size_t count)   /* cio_fil
 
 int cioa_chunk_write_at(cioa_chunk *ch, off_t offset, const void *buf, size_t count)  /* cio_chunk.c:184-209 */
 {
+    settle(ch);
     if (!ch) {
         return -1;
     }
@@ -877,6 +884,7 @@ static int adjust_layout(cioa_chunk *ch, size_t meta_size)  /* cio_file.c:130-14
 
 int cioa_meta_write(cioa_chunk *ch, const char *buf, size_t size)    /* cio_meta.c:46-73 */
 {
+    settle(ch);
     if (!ch || size > 65535) {
         return -1;
     }
@@ -987,33 +995,80 @@ static int sync_commit(cioa_chunk *ch)
     return update_size(ch) == CIO_OK ? 0 : -1;
 }
 
-int cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n)
+struct cioa_sync_job {
+    cio_sync_job *fjob;          /* the CRC pass (cio_sync.c), NULL when none started */
+    cio_sync_item *items;
+    cioa_chunk **bat;
+    size_t m;
+    int rc;
+    int done;                    /* finished: headers written, chunks released */
+};
+
+/* Wait for the batch's CRC pass and commit it (headers, msyncs, synced
+ * flags); releases its chunks.  Runs once; the job stays for end(). */
+static void job_finish(cioa_sync_job *job)
 {
-    int rc = CIO_OK;
-    size_t m = 0;
-    cio_sync_item *items = NULL;
-    cioa_chunk **bat = NULL;
-    if (n == 0) {
-        return CIO_OK;
+    if (job->done) {
+        return;
     }
-    items = calloc(n, sizeof(*items));
-    bat = calloc(n, sizeof(*bat));
-    if (!items || !bat) {
-        free(items);
-        free(bat);
+    job->done = 1;
+    const int crc_ok = job->fjob && cio_file_sync_batch_end(job->fjob) == CIO_OK;
+    job->fjob = NULL;
+    for (size_t k = 0; k < job->m; k++) {
+        cioa_chunk *ch = job->bat[k];
+        ch->pending = NULL;
+        if (!crc_ok) {
+            job->rc = CIO_ERROR;
+            continue;
+        }
+        if (job->items[k].status != CIO_OK) {
+            error_set(ch, CIO_ERR_BAD_LAYOUT);
+            job->rc = CIO_ERROR;
+            continue;
+        }
+        ch->crc_cur = job->items[k].crc_cur;
+        ch->crc_end = job->items[k].crc_end;
+        if (sync_commit(ch) != 0) {
+            job->rc = CIO_ERROR;
+        }
+    }
+}
+
+/* A chunk held by a begun batch sync: finish that batch first. */
+static void settle(cioa_chunk *ch)
+{
+    if (ch && ch->pending) {
+        job_finish(ch->pending);
+    }
+}
+
+int cioa_chunk_sync_batch_begin(cioa_chunk **chunks, size_t n, cioa_sync_job **out)
+{
+    if (!out) {
+        return CIO_ERROR;
+    }
+    *out = NULL;
+    cioa_sync_job *job = calloc(1, sizeof(*job));
+    if (!job || (n > 0 && (!(job->items = calloc(n, sizeof(*job->items))) ||
+                           !(job->bat = calloc(n, sizeof(*job->bat)))))) {
+        if (job) {
+            free(job->items);
+            free(job);
+        }
         return CIO_ERROR;
     }
     cioa_ctx *ctx = NULL;
     for (size_t i = 0; i < n; i++) {
         cioa_chunk *ch = chunks[i];
         size_t file_size;
-        if (!ch) {
+        if (!ch || ch->pending == job) {       /* (listed twice: already in this batch) */
             continue;
         }
+        settle(ch);
         ch->error_n = 0;
         const int need = sync_prepare(ch, &file_size);
         if (need < 0) {
-            rc = CIO_ERROR;
+            job->rc = CIO_ERROR;
             continue;
         }
         if (need == 0) {
@@ -1022,18 +1077,19 @@ int cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n)
         if (deferred(ch)) {
             if (ch->crc_reset) {
                 if (full_recompute(ch) != CIO_OK) {
-                    rc = CIO_ERROR;
+                    job->rc = CIO_ERROR;
                     continue;
                 }
                 ch->crc_reset = 0;
             }
-            cio_sync_item *it = &items[m];
+            cio_sync_item *it = &job->items[job->m];
             it->map = ch->map;
             it->fs_size = ch->alloc_size;
             it->crc_end = ch->crc_end;
             it->crc_cur = ch->crc_cur;
             it->data_end = region_end(ch);
-            bat[m++] = ch;
+            job->bat[job->m++] = ch;
+            ch->pending = job;
             ctx = ch->ctx;
             continue;
         }
@@ -1042,34 +1098,42 @@ int cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n)
             memcpy(ch->map + 2, &crc, sizeof(crc));
         }
         if (sync_commit(ch) != 0) {
-            rc = CIO_ERROR;
+            job->rc = CIO_ERROR;
         }
     }
-    if (m > 0) {
-        /* one GPU pass for every deferred chunk: CRC of [crc_end, end) seeded
-         * with crc_cur, finalized header written; msync below */
-        if (cio_file_sync_batch_multi(items, m, CIOA_SYNC_FINALIZE, ctx->devs, ctx->ndev) != CIO_OK) {
-            rc = CIO_ERROR;
-        }
-        else {
-            for (size_t k = 0; k < m; k++) {
-                cioa_chunk *ch = bat[k];
-                if (items[k].status != CIO_OK) {
-                    error_set(ch, CIO_ERR_BAD_LAYOUT);
-                    rc = CIO_ERROR;
-                    continue;
-                }
-                ch->crc_cur = items[k].crc_cur;
-                ch->crc_end = items[k].crc_end;
-                if (sync_commit(ch) != 0) {
-                    rc = CIO_ERROR;
-                }
-            }
-        }
+    /* one pass for every deferred chunk: CRC of [crc_end, end) seeded with
+     * crc_cur, on its own thread; the finalized headers and msyncs at the end */
+    if (job->m > 0 &&
+        cio_file_sync_batch_begin(job->items, job->m, CIOA_SYNC_FINALIZE, ctx->devs, ctx->ndev, &job->fjob) != CIO_OK) {
+        job->rc = CIO_ERROR;
     }
-    free(items);
-    free(bat);
+    *out = job;
+    return CIO_OK;
+}
+
+int cioa_chunk_sync_batch_end(cioa_sync_job *job)
+{
+    if (!job) {
+        return CIO_ERROR;
+    }
+    job_finish(job);
+    const int rc = job->rc;
+    free(job->items);
+    free(job->bat);
+    free(job);
     return rc;
+}
+
+int cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n)
+{
+    if (n == 0) {
+        return CIO_OK;
+    }
+    cioa_sync_job *job;
+    if (cioa_chunk_sync_batch_begin(chunks, n, &job) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    return cioa_chunk_sync_batch_end(job);
 }
 
 int cioa_chunk_sync(cioa_chunk *ch)
@@ -1206,6 +1270,7 @@ int cioa_chunk_is_locked(cioa_chunk *ch)
 
 int cioa_chunk_tx_begin(cioa_chunk *ch)
 {
+    settle(ch);
     ch->error_n = 0;
     if (cioa_chunk_is_locked(ch)) {
         return CIO_RETRY;
@@ -1225,6 +1290,7 @@ int cioa_chunk_tx_begin(cioa_chunk *ch)
 
 int cioa_chunk_tx_commit(cioa_chunk *ch)
 {
+    settle(ch);
     ch->error_n = 0;
     if (cioa_chunk_sync(ch) == -1) {
         return CIO_ERROR;
@@ -1235,6 +1301,7 @@ int cioa_chunk_tx_commit(cioa_chunk *ch)
 
 int cioa_chunk_tx_rollback(cioa_chunk *ch)
 {
+    settle(ch);
     ch->error_n = 0;
     if (!ch->tx_active) {
         return -1;
@@ -1290,6 +1357,7 @@ int cioa_chunk_up_force(cioa_chunk *ch)
 
 int cioa_chunk_down(cioa_chunk *ch)
 {
+    settle(ch);
     ch->error_n = 0;
     if (!ch->map) {
         return -1;
@@ -1584,14 +1652,14 @@ int cioa_bench_perf_write(const char *root, const void *data, size_t len, int fi
 {
     char name[64];
     struct timespec t1, t2;
-    cioa_ctx *ctx = cioa_create(root, flags);
+    cioa_ctx *ctx = cioa_create(root, flags & ~CIOA_BENCH_PIPELINED_SYNC);
     if (!ctx) {
         return CIO_ERROR;
     }
     if (batch < 1) {
         batch = 1;
     }
-    cioa_set_max_chunks_up(ctx, batch + CIOA_MAX_CHUNKS_UP);
+    cioa_set_max_chunks_up(ctx, 2 * batch + CIOA_MAX_CHUNKS_UP);
     cioa_stream *st = cioa_stream_create(ctx, "test-perf");
     cioa_chunk **group = calloc((size_t) batch, sizeof(*group));
     if (!st || !group) {
@@ -1600,6 +1668,15 @@ int cioa_bench_perf_write(const char *root, const void *data, size_t len, int fi
         return CIO_ERROR;
     }
     const int defer = (flags & CIOA_DEFERRED_CRC) && (flags & CIO_CHECKSUM);
+    const int pipelined = defer && (flags & CIOA_BENCH_PIPELINED_SYNC);
+    cioa_chunk **prev = pipelined ? calloc((size_t) batch, sizeof(*prev)) : NULL;
+    cioa_sync_job *job = NULL;
+    int nprev = 0;
+    if (pipelined && !prev) {
+        free(group);
+        cioa_destroy(ctx);
+        return CIO_ERROR;
+    }
     uint64_t nb = 0;
     int rc = CIO_OK, ng = 0, err;
     clock_gettime(CLOCK_REALTIME, &t1);
@@ -1622,7 +1699,10 @@ int cioa_bench_perf_write(const char *root, const void *data, size_t len, int fi
             continue;
         }
         group[ng++] = ch;
-        if (ng == batch || i == files - 1) {
+        if (ng < batch && i < files - 1) {
+            continue;
+        }
+        if (!pipelined) {
             if (cioa_chunk_sync_batch(group, (size_t) ng) != CIO_OK) {
                 rc = CIO_ERROR;
             }
@@ -1630,12 +1710,37 @@ int cioa_bench_perf_write(const char *root, const void *data, size_t len, int fi
                 cioa_chunk_close(group[k], 0);
             }
             ng = 0;
+            continue;
         }
+        /* pipelined: this group's CRC pass starts, the previous group's ends
+         * (headers, msyncs) and its chunks close; the next group's writes
+         * overlap this group's pass */
+        cioa_sync_job *cur = NULL;
+        if (cioa_chunk_sync_batch_begin(group, (size_t) ng, &cur) != CIO_OK) {
+            rc = CIO_ERROR;
+        }
+        if (job && cioa_chunk_sync_batch_end(job) != CIO_OK) {
+            rc = CIO_ERROR;
+        }
+        for (int k = 0; k < nprev; k++) {
+            cioa_chunk_close(prev[k], 0);
+        }
+        job = cur;
+        memcpy(prev, group, (size_t) ng * sizeof(*group));
+        nprev = ng;
+        ng = 0;
+    }
+    if (job && cioa_chunk_sync_batch_end(job) != CIO_OK) {
+        rc = CIO_ERROR;
+    }
+    for (int k = 0; k < nprev; k++) {
+        cioa_chunk_close(prev[k], 0);
     }
     for (int k = 0; k < ng; k++) {
         cioa_chunk_close(group[k], 0);
     }
     clock_gettime(CLOCK_REALTIME, &t2);
+    free(prev);
     free(group);
     cioa_destroy(ctx);
     if (secs) {

@@ -64,6 +64,19 @@ int cio_file_sync_batch(cio_sync_item *items, size_t n, int flags);
 int cio_file_sync_batch_multi(cio_sync_item *items, size_t n, int flags,
                               const int *devices, int ndev);
 
+/* The same batch with the CRC pass on a thread of its own, so the caller can
+ * go on (e.g. write the next chunks) while it runs.  begin() checks the
+ * headers and starts the pass (on the devices given, else the caller's
+ * current device); end() waits for it, writes the headers, runs the msyncs and
+ * frees the job.  Between the two the items and the mapped bytes they cover
+ * must stay as they are.  begin() returns CIO_ERROR with *job = NULL only when
+ * nothing started (no memory); end() returns what cio_file_sync_batch_multi
+ * returns.  Every job begun must be ended. */
+typedef struct cio_sync_job cio_sync_job;
+int cio_file_sync_batch_begin(cio_sync_item *items, size_t n, int flags,
+                              const int *devices, int ndev, cio_sync_job **job);
+int cio_file_sync_batch_end(cio_sync_job *job);
+
 #ifdef __cplusplus
 }
 #endif

@@ -163,6 +163,18 @@ int  cioa_chunk_sync(cioa_chunk *ch);
  * deferred CRCs of all of them in ONE GPU pass.  CIO_OK when every chunk
  * synced; otherwise CIO_ERROR (chunks that failed stay unsynced). */
 int  cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n);
+/* The same in two halves, so the caller can go on while the CRC pass runs on
+ * a thread of its own (cio_file_sync_batch_begin/end): begin() syncs the
+ * chunks that need no CRC pass and starts the pass over the deferred ones;
+ * end() waits for it, writes the finalized headers, msyncs and marks the
+ * chunks synced, returns what cioa_chunk_sync_batch would have and frees the
+ * job.  Until then a chunk of the batch is held: writing, syncing, a metadata
+ * write, a transaction, down or close of it finishes the whole batch first
+ * (the job stays valid for end()).  begin() fails (*job = NULL) only without
+ * memory; every job begun must be ended (also after its context is gone). */
+typedef struct cioa_sync_job cioa_sync_job;
+int  cioa_chunk_sync_batch_begin(cioa_chunk **chunks, size_t n, cioa_sync_job **job);
+int  cioa_chunk_sync_batch_end(cioa_sync_job *job);
 int  cioa_chunk_get_content(cioa_chunk *ch, char **buf, size_t *size);
 int  cioa_chunk_get_content_copy(cioa_chunk *ch, void **out_buf, size_t *out_size);
 ssize_t cioa_chunk_get_content_size(cioa_chunk *ch);
@@ -203,6 +215,11 @@ int  cioa_meta_size(cioa_chunk *ch);
  * loop, *bytes = bytes written (files * writes * len). */
 int cioa_bench_perf_write(const char *root, const void *data, size_t len, int files, int writes,
                           int batch, int flags, double *secs, uint64_t *bytes);
+/* flags bit for cioa_bench_perf_write only (not a context flag): with
+ * CIOA_DEFERRED_CRC, each batch's CRC pass runs while the next batch is
+ * written (cioa_chunk_sync_batch_begin / _end), the batch before it ended and
+ * closed when the next begins. */
+#define CIOA_BENCH_PIPELINED_SYNC 0x10000
 
 #ifdef __cplusplus
 }

@@ -755,27 +755,96 @@ static void test_identity_corpus(void)
 }
 
 /* The `tools/cio -k -p` loop through the benchmark driver: 20 files, the
- * reference's perf-file header on every one. */
+ * reference's perf-file header on every one; in deferred mode also with each
+ * batch's CRC pass overlapping the next batch's writes. */
 static void test_perf_driver(void)
 {
     char path[4096];
     double secs;
     uint64_t bytes;
-    env_path(path, sizeof(path), "perf");
-    rm_rf(path);
-    TEST_CHECK(cioa_bench_perf_write(path, in_data, in_size, 20, 5, 8, CIO_CHECKSUM | g_mode, &secs,
-                                     &bytes) == CIO_OK);
-    TEST_CHECK(bytes == 20 * 5 * in_size);
-    for (int i = 0; i < 20; i++) {
-        char name[128];
-        size_t n;
-        snprintf(name, sizeof(name), "perf/test-perf/perf-test-%04d.txt", i);
-        env_path(path, sizeof(path), name);
-        unsigned char *raw = slurp(path, &n);
-        TEST_CHECK(raw && n == 2068480 &&
-                   memcmp(raw, "\xc1\x00\x08\x87\x40\xe7\x00\x00\x00\x00\x00\x1f\x40\x00", 14) == 0);
-        free(raw);
+    for (int pipelined = 0; pipelined <= (g_mode ? 1 : 0); pipelined++) {
+        env_path(path, sizeof(path), "perf");
+        rm_rf(path);
+        TEST_CHECK(cioa_bench_perf_write(path, in_data, in_size, 20, 5, 8,
+                                         CIO_CHECKSUM | g_mode | (pipelined ? CIOA_BENCH_PIPELINED_SYNC : 0),
+                                         &secs, &bytes) == CIO_OK);
+        TEST_CHECK(bytes == 20 * 5 * in_size);
+        for (int i = 0; i < 20; i++) {
+            char name[128];
+            size_t n;
+            snprintf(name, sizeof(name), "perf/test-perf/perf-test-%04d.txt", i);
+            env_path(path, sizeof(path), name);
+            unsigned char *raw = slurp(path, &n);
+            TEST_CHECK(raw && n == 2068480 &&
+                       memcmp(raw, "\xc1\x00\x08\x87\x40\xe7\x00\x00\x00\x00\x00\x1f\x40\x00", 14) == 0);
+            free(raw);
+        }
     }
+}
+
+/* cioa_chunk_sync_batch_begin / _end: three groups of chunks, each group's
+ * CRC pass running while the next group is written; a write to a held chunk
+ * and a close of one finish their batch first.  The files and crc_cur equal
+ * those of the same operations synced by cioa_chunk_sync_batch. */
+static void test_sync_batch_async(void)
+{
+    int err;
+    char name[64], path[4096];
+    uint32_t want[60], got[60];
+    for (int pass = 0; pass < 2; pass++) {
+        cioa_ctx *ctx = ctx_new(pass ? "async-b" : "async-a", CIO_CHECKSUM);
+        cioa_set_max_chunks_up(ctx, 256);
+        cioa_stream *st = cioa_stream_create(ctx, "s");
+        cioa_chunk *arr[60];
+        cioa_sync_job *job[3] = {NULL, NULL, NULL};
+        for (int g = 0; g < 3; g++) {
+            for (int i = 20 * g; i < 20 * g + 20; i++) {
+                snprintf(name, sizeof(name), "c%02d", i);
+                arr[i] = cioa_chunk_open(ctx, st, name, CIO_OPEN, 0, &err);
+                TEST_CHECK(arr[i] != NULL);
+                if (i % 7 == 0) {
+                    cioa_meta_write(arr[i], name, strlen(name));
+                }
+                cioa_chunk_write(arr[i], in_data + i * 131, (size_t) (i * 7919) % 300000 + 1);
+            }
+            if (pass == 0) {
+                TEST_CHECK(cioa_chunk_sync_batch(arr + 20 * g, 20) == CIO_OK);
+            }
+            else {
+                TEST_CHECK(cioa_chunk_sync_batch_begin(arr + 20 * g, 20, &job[g]) == CIO_OK && job[g]);
+            }
+        }
+        /* a write to a held chunk (group 2) and a close (group 1) */
+        TEST_CHECK(cioa_chunk_write(arr[45], "tail", 4) == 0);
+        TEST_CHECK(cioa_chunk_sync(arr[45]) == 0);
+        if (pass == 1) {
+            cioa_chunk_close(arr[30], 0);
+            for (int g = 0; g < 3; g++) {
+                TEST_CHECK(cioa_chunk_sync_batch_end(job[g]) == CIO_OK);
+            }
+        }
+        for (int i = 0; i < 60; i++) {     /* (held chunks' crc_cur is current after end) */
+            (pass ? got : want)[i] = (pass && i == 30) ? want[30] : cioa_chunk_crc_cur(arr[i]);
+        }
+        cioa_destroy(ctx);
+    }
+    int diff = 0;
+    for (int i = 0; i < 60; i++) {
+        size_t n1, n2;
+        snprintf(name, sizeof(name), "async-a/s/c%02d", i);
+        env_path(path, sizeof(path), name);
+        unsigned char *a = slurp(path, &n1);
+        snprintf(name, sizeof(name), "async-b/s/c%02d", i);
+        env_path(path, sizeof(path), name);
+        unsigned char *b = slurp(path, &n2);
+        if (!a || !b || n1 != n2 || memcmp(a, b, n1) != 0 || want[i] != got[i]) {
+            diff++;
+            fprintf(stderr, "  async: c%02d differs\n", i);
+        }
+        free(a);
+        free(b);
+    }
+    TEST_CHECK(diff == 0);
 }
 
 struct test {
@@ -804,6 +873,7 @@ static const struct test tests[] = {
     {"sync_batch_and_scan", test_sync_batch_and_scan},
     {"identity_corpus", test_identity_corpus},
     {"perf_driver", test_perf_driver},
+    {"sync_batch_async", test_sync_batch_async},
     {NULL, NULL},
 };
 

@@ -377,6 +377,88 @@ def test_deferred_crc_perf_files_and_reopen_append(route, tmp_path, data400):
 
 
 @pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_sync_batch_begin_end_overlaps_the_next_writes(route, tmp_path):
+    """cioa_chunk_sync_batch_begin / _end: a batch's CRC pass runs on its own
+    thread while the next chunks are written; every file ends byte-identical
+    to the reference's write/sync path."""
+    rng = np.random.default_rng(43)
+    ref_dir, def_dir = tmp_path / "ref", tmp_path / "deferred"
+    ref_dir.mkdir()
+    def_dir.mkdir()
+    ctx = cf.Context(str(tmp_path / "ctx"), cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, max_chunks_up=200)
+    st = ctx.stream("s")
+    jobs, groups, want = [], [], []
+    for g in range(3):
+        group = []
+        for i in range(20):
+            ops = _ops(rng)
+            a, _ = cf.ChunkFile.open(str(ref_dir / f"c{g}{i:02d}"))
+            _apply(a, ops)
+            a.sync()
+            want.append(a.crc_cur)
+            a.close()
+            c, _ = st.open(f"c{g}{i:02d}")
+            _apply(c, ops)
+            group.append(c)
+        jobs.append(cf.sync_batch_begin(group))      # pass g runs while group g+1 is written
+        groups.append(group)
+    crcs = []
+    for job, group in zip(jobs, groups):
+        assert job.end() == cf.CIO_OK
+        crcs += [c.crc_cur for c in group]
+    for g in range(3):
+        for i in range(20):
+            n = f"c{g}{i:02d}"
+            assert open(tmp_path / "ctx" / "s" / n, "rb").read() == open(ref_dir / n, "rb").read(), n
+    assert crcs == want
+    ctx.close()
+
+
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_pending_batch_finishes_before_its_chunks_change(route, tmp_path, data400):
+    """A chunk held by a begun batch: writing it, syncing it, a transaction,
+    down or close finishes the whole batch first; end() afterwards returns
+    the batch's result and frees it."""
+    ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, max_chunks_up=100)
+    st = ctx.stream("s")
+    cs = [st.open(f"p{i}")[0] for i in range(6)]
+    for c in cs:
+        c.write(data400)
+    job = cf.sync_batch_begin(cs)
+    assert cs[0].write(b"more") == 0                  # finishes the batch, then appends
+    for c in cs[1:]:                                   # the rest were synced by that
+        assert bytes(c.map[:10]).hex() == "c100" + "103cfa67" + "00000000"
+    cs[2].close()                                      # no pending batch any more
+    assert job.end() == cf.CIO_OK
+    job2 = cf.sync_batch_begin([cs[0], cs[1]])
+    cs[1].down()
+    cs[0].close()                                      # closing a held chunk finishes the batch
+    assert job2.end() == cf.CIO_OK
+    job3 = cf.sync_batch_begin([])                     # nothing to do
+    assert job3.end() == cf.CIO_OK
+    ctx.close()
+    st2, er, crc = cf.verify_paths([str(tmp_path / "s" / f"p{i}") for i in range(6)])
+    assert list(st2) == [cf.CIO_OK] * 6
+    assert int(crc[0]) == po.crc_update(INIT, b"\0\0" + data400 + b"more")
+
+
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_perf_write_pipelined_sync(route, tmp_path, data400):
+    """cioa_bench_perf_write with CIOA_BENCH_PIPELINED_SYNC writes the same
+    files as the plain deferred loop (batches of 7 over 30 files: a short
+    last batch, every batch's pass overlapping the next batch's writes)."""
+    out = {}
+    for tag, extra in (("plain", 0), ("pipelined", cf.CIOA_BENCH_PIPELINED_SYNC)):
+        root = tmp_path / tag
+        secs, nb = cf.perf_write(str(root), data400, files=30, writes=5, batch=7,
+                                 flags=cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC | extra)
+        assert nb == 30 * 5 * len(data400) and secs > 0
+        out[tag] = {n: open(root / "test-perf" / n, "rb").read() for n in sorted(os.listdir(root / "test-perf"))}
+    assert len(out["plain"]) == 30 and out["plain"] == out["pipelined"]
+    assert all(b[:10].hex() == "c100088740e700000000" for b in out["pipelined"].values())
+
+
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
 def test_sync_batch_rejects_bad_items(route, tmp_path):
     import ctypes
     import mmap

@@ -19,15 +19,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--batch", type=int, default=100)
-    ap.add_argument("--legs", default="nocrc,immediate,deferred,deferred_host")
+    ap.add_argument("--legs", default="nocrc,immediate,deferred,deferred_async,deferred_host,deferred_async_host")
     args = ap.parse_args()
     import chunkio_amd as cio
     from chunkio_amd import chunkfile as cf
     d400 = open(os.path.join(ROOT, "tests", "golden", "400kb.txt"), "rb").read()
     legs = {"nocrc": (0, None), "immediate": (cf.CIO_CHECKSUM, None),
             "deferred": (cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, None),
-            "deferred_async": (cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC | getattr(cf, "CIOA_PERF_ASYNC_SYNC", 0), None),
-            "deferred_host": (cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, 16)}
+            "deferred_async": (cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC | cf.CIOA_BENCH_PIPELINED_SYNC, None),
+            "deferred_host": (cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, 16),
+            "deferred_async_host": (cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC | cf.CIOA_BENCH_PIPELINED_SYNC, 16)}
     res = {k: [] for k in args.legs.split(",")}
     root = tempfile.mkdtemp(prefix="cioa-ceil-")
     try:
