@@ -1087,6 +1087,12 @@ def run_perf(args, rank, world, device, dist, compact=False):
         return min(times), nb, hdr_ok
 
     t_def, nbytes, ok_def = timed(cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC, "deferred")
+    # the same with each batch's CRC pass on its own thread while the next
+    # batch is written (cioa_chunk_sync_batch_begin / _end)
+    t_pipe, _, ok_pipe = timed(cf.CIO_CHECKSUM | cf.CIOA_DEFERRED_CRC | cf.CIOA_BENCH_PIPELINED_SYNC, "pipelined")
+    pipelined = {"GBps": round(nbytes / t_pipe / 1e9, 3), "ms": round(t_pipe * 1e3, 2),
+                 "note": "deferred CRC, each 100-chunk sync batch's pass (default route) overlapping the next "
+                         "batch's writes: cioa_chunk_sync_batch_begin / _end"}
     # The same C layer in the reference's order (crc_update per write on the
     # calling thread: VPCLMULQDQ folding over the cached 400 KB buffer), and
     # deferred with the sync batches on the host (host threads granted, so the
@@ -1118,8 +1124,8 @@ def run_perf(args, rank, world, device, dist, compact=False):
                 "config": {"workload": "config 1 loop through the C chunk layer (cioa_bench_perf_write): open, "
                                        "5 x write 409600 B, sync (batches of 100 chunks per GPU pass), close",
                            "files": files, "writes": writes, "sync_batch": batch},
-                "host_paths": host_paths,
-                "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm and ok_dh)},
+                "pipelined_sync": pipelined, "host_paths": host_paths,
+                "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm and ok_dh and ok_pipe)},
                 "cpu_baseline_ref": "cpu_baseline.cio_perf_k_p of this line: the reference loop with the "
                                     "reference's own crc_update, same box, same run"}
     from oracle import pyoracle as po
@@ -1144,8 +1150,8 @@ def run_perf(args, rank, world, device, dist, compact=False):
             "config": {"workload": "config 1 loop through the C chunk layer (cioa_bench_perf_write): open, "
                                    "5 x write 409600 B, sync (batches of 100 chunks per GPU pass), close",
                        "files": files, "writes": writes, "sync_batch": batch},
-            "host_paths": host_paths,
-            "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm and ok_dh)},
+            "pipelined_sync": pipelined, "host_paths": host_paths,
+            "check": {"last_file_header_c100088740e7": bool(ok_def and ok_imm and ok_dh and ok_pipe)},
             "vs_baseline_note": "BASELINE.md's published `cio -k -p` rate, 545,507,660 B/s (README.md:120-129, "
                                 "hardware unstated)",
             "cpu_baseline": {"value": ref["crc_on"]["GBps"], "unit": "GB/s", "cores": 1, "kind": kind,
