@@ -1509,7 +1509,7 @@ def other_configs(args, rank, world, device, dist, only=None):
         keep = {k: r[k] for k in ("metric", "value", "unit", "scaling", "steps", "warmup", "ms_per_step")}
         keep["workload"] = r["config"].get("workload")
         for k in ("roofline", "check", "per_gpu", "registered_in_place", "breakdown", "pipe_legs_last_call",
-                  "host_cpu_batch", "host_route", "host_paths", "numa", "staged_call_ms",
+                  "host_cpu_batch", "host_route", "host_paths", "pipelined_sync", "numa", "staged_call_ms",
                   "cpu_baseline", "cpu_baseline_ref", "vs_baseline", "vs_baseline_note"):
             if k in r:
                 keep[k] = r[k]
