@@ -81,6 +81,13 @@ def main():
         print("   WG entry spread (last-first wave)", q(ent.max(1) - ent.min(1)))
         print("   WG first entry                   ", q(ent.min(1)))
         print("   WG tables - last entry           ", q(tab.max(1) - ent.max(1)))
+        iss = us[:, 6].reshape(-1, 16)
+        bld = us[:, 7].reshape(-1, 16)
+        print("   WG issued spread (last-first)    ", q(iss.max(1) - iss.min(1)))
+        print("   WG build spread (last-first)     ", q(bld.max(1) - bld.min(1)))
+        print("   WG tables - WG last build        ", q(tab.max(1) - bld.max(1)))
+        print("   WG tables - WG first build       ", q(tab.max(1) - bld.min(1)))
+        print("   issued - entry by wave slot", " ".join(f"{x:5.2f}" for x in (iss - ent).mean(0)))
         wg = us[:, 2].reshape(-1, 16)
         print("   WG max done", q(wg.max(1)))
         print("   WG min done", q(wg.min(1)))
