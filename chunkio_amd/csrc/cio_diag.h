@@ -33,7 +33,8 @@
 #endif
 
 /* Diagnostic: skip the arrival/fold step of split chunks (prices the tail;
- * wrong CRCs for split chunks). */
+ * wrong CRCs for split chunks).  2: also skip the arrival descriptors' loads
+ * at kernel start (prices their share of the start-up). */
 #ifndef CIO_DIAG_NO_ARRIVAL
 #define CIO_DIAG_NO_ARRIVAL 0
 #endif

@@ -816,9 +816,9 @@ crc32_stream_kernel(const uint8_t *base, uint64_t S, uint64_t ustride, uint64_t 
     // Descriptors of the first 64 chunks from c0 (one per lane) for the
     // arrival step at the end; fetched now so that they cost nothing there.
     // Clamped, not predicated: a branch would break the ring's vmcnt tracking.
-    uint64_t ar_g;
-    uint32_t ar_ns, ar_np, ar_w0, ar_w1;
-    {
+    uint64_t ar_g = 0;
+    uint32_t ar_ns = 0, ar_np = 0, ar_w0 = 0, ar_w1 = 0;
+    if (CIO_DIAG_NO_ARRIVAL < 2) {
         const ChunkDesc &ad = desc[min(c0 + lane, n - 1)];
         ar_g = ad.g;
         ar_ns = ad.nsteps;
