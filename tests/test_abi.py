@@ -198,6 +198,21 @@ def test_sha1_entry_points_reject_null_pointers_without_a_gpu():
     assert b"null pointer" in lib.cio_gpu_last_error()
 
 
+def test_plan_create_rejects_bad_arguments_without_a_gpu():
+    """cio_crc32_plan_create checks its arguments before any device call:
+    null arrays and 2^32 or more chunks are CIO_ERROR with a message."""
+    lib = chunkio_amd.lib()
+    h = ctypes.c_void_p()
+    offs = (ctypes.c_uint64 * 1)(0)
+    assert lib.cio_crc32_plan_create(None, offs, offs, 1) == -1
+    assert b"null argument" in lib.cio_gpu_last_error()
+    assert lib.cio_crc32_plan_create(ctypes.byref(h), None, offs, 1) == -1
+    assert b"null argument" in lib.cio_gpu_last_error()
+    assert lib.cio_crc32_plan_create(ctypes.byref(h), offs, offs, 1 << 32) == -1
+    assert b"too many chunks" in lib.cio_gpu_last_error()
+    assert not h.value
+
+
 def test_library_shares_torchs_hip_runtime_when_loaded_first():
     """Loaded before torch, the library must bind torch's libamdhip64 (not a
     second copy from /opt/rocm): two HIP/HSA runtimes in one process leave the

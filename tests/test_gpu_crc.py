@@ -369,6 +369,21 @@ def test_chunk_longer_than_4gib(cuda):
     assert [int(x) for x in got] == want
 
 
+def test_plan_create_refuses_geometry_past_its_limits(cuda):
+    """A chunk of more than 2^32 - 1 wave-steps (16 TiB) and a batch of 2^40
+    wave-steps or more are refused at plan creation with a message; nothing is
+    allocated for them (the lengths are never backed by memory)."""
+    import ctypes
+    lib = cio.lib()
+    for lens, msg in (([1 << 45], b"chunk too large"), ([1 << 43] * 512, b"batch too large")):
+        offs = (ctypes.c_uint64 * len(lens))(*([0] * len(lens)))
+        ln = (ctypes.c_uint64 * len(lens))(*lens)
+        h = ctypes.c_void_p()
+        assert lib.cio_crc32_plan_create(ctypes.byref(h), offs, ln, len(lens)) == -1
+        assert msg in lib.cio_gpu_last_error()
+        assert not h.value
+
+
 def test_plan_reuse_on_stream(cuda):
     import torch
     lens = wl.cfg2_lens(64)
