@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-5 GPU session af: GPU suite (new limit tests), smoke and the driver's
+# default line on the final tree.
+set -u
+O=gpurun_out/${1:-r05af}
+mkdir -p $O
+export TMPDIR=/tmp
+step() { local rc=$1 what=$2; echo "[$what] rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stop after $what"; exit "$rc"; fi; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
+    --timeout 120 --timeout-method thread > $O/pytest_gpu.txt 2>&1; step $? pytest
+tail -1 $O/pytest_gpu.txt
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1; step $? smoke
+timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err; step $? default
+echo all-done
