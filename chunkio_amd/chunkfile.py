@@ -96,6 +96,9 @@ def _bind():
         "cio_file_sync_batch_begin": (I, [ctypes.POINTER(SyncItem), S, I, IP, I, ctypes.POINTER(V)]),
         "cio_file_sync_batch_end": (I, [V]),
         "cioa_chunk_get_content_size": (ctypes.c_ssize_t, [V]),
+        "cioa_chunk_get_content_end_pos": (S, [V]),
+        "cioa_chunk_is_file": (I, [V]),
+        "cioa_chunk_close_stream": (None, [V]),
         "cioa_chunk_get_real_size": (ctypes.c_ssize_t, [V]),
         "cioa_chunk_hash": (V, [V]),
         "cioa_chunk_map": (V, [V, ctypes.POINTER(S)]),
@@ -258,6 +261,13 @@ class Stream:
     def size_chunks_up(self):
         return int(self.ctx._lib.cioa_stream_size_chunks_up(self._h))
 
+    def close_chunks(self):
+        """cioa_chunk_close_stream: close every chunk of the stream (files kept)."""
+        chunks = self.chunks()
+        self.ctx._lib.cioa_chunk_close_stream(self._h)
+        for c in chunks:
+            c._h = None
+
 
 class Chunk:
     """cio_chunk over the C layer."""
@@ -328,6 +338,13 @@ class Chunk:
     @property
     def data_size(self):
         return int(self._lib.cioa_chunk_get_content_size(self._c()))
+
+    @property
+    def content_end_pos(self):
+        return int(self._lib.cioa_chunk_get_content_end_pos(self._c()))
+
+    def is_file(self):
+        return bool(self._lib.cioa_chunk_is_file(self._c()))
 
     @property
     def real_size(self):

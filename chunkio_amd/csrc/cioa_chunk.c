@@ -1191,6 +1191,37 @@ ssize_t cioa_chunk_get_content_size(cioa_chunk *ch)
     return ch ? (ssize_t) ch->data_size : -1;
 }
 
+/* cio_chunk_get_content_end_pos (src/cio_chunk.c:293-313): the address just
+ * past the content, as a number; 0 for a chunk that is down (the reference
+ * would read the header through a NULL map there). */
+size_t cioa_chunk_get_content_end_pos(cioa_chunk *ch)
+{
+    if (!ch || !ch->map) {
+        return 0;
+    }
+    ch->error_n = 0;
+    return (size_t) (uintptr_t) (ch->map + CIOA_HDR_MIN + cioa_st_meta_len(ch->map) + ch->data_size);
+}
+
+/* cio_chunk_is_file (src/cio_chunk.c:526-536): every chunk of this layer is
+ * file-backed (the memory backend is out of scope). */
+int cioa_chunk_is_file(cioa_chunk *ch)
+{
+    return ch ? 1 : 0;
+}
+
+/* cio_chunk_close_stream (src/cio_chunk.c:363-373): close every chunk of the
+ * stream, keeping their files. */
+void cioa_chunk_close_stream(cioa_stream *st)
+{
+    if (!st) {
+        return;
+    }
+    while (st->head) {
+        cioa_chunk_close(st->head, 0);
+    }
+}
+
 ssize_t cioa_chunk_get_real_size(cioa_chunk *ch)
 {
     if (!ch) {

@@ -178,6 +178,9 @@ int  cioa_chunk_sync_batch_end(cioa_sync_job *job);
 int  cioa_chunk_get_content(cioa_chunk *ch, char **buf, size_t *size);
 int  cioa_chunk_get_content_copy(cioa_chunk *ch, void **out_buf, size_t *out_size);
 ssize_t cioa_chunk_get_content_size(cioa_chunk *ch);
+size_t  cioa_chunk_get_content_end_pos(cioa_chunk *ch);   /* address past the content; 0 when down */
+int  cioa_chunk_is_file(cioa_chunk *ch);                  /* 1: every chunk here is file-backed */
+void cioa_chunk_close_stream(cioa_stream *st);            /* close every chunk, files kept */
 ssize_t cioa_chunk_get_real_size(cioa_chunk *ch);
 char *cioa_chunk_hash(cioa_chunk *ch);        /* map + 2, NULL when down */
 int  cioa_chunk_lock(cioa_chunk *ch);

@@ -99,6 +99,28 @@ def test_cio_perf_file_bytes(tmp_path, data400):
     assert open(d / "perf-test-0000.txt", "rb").read() == open(p, "rb").read()
 
 
+def test_content_end_pos_is_file_and_close_stream(tmp_path, data400):
+    """cio_chunk_get_content_end_pos / cio_chunk_is_file / cio_chunk_close_stream
+    (src/cio_chunk.c:293-313, 526-536, 363-373): the address past the content,
+    a file-backed chunk, and every chunk of a stream closed with its file kept."""
+    import ctypes
+    ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM)
+    st = ctx.stream("s")
+    cs = [st.open(f"c{i}")[0] for i in range(3)]
+    cs[1].meta_write(b"meta!")
+    for i, c in enumerate(cs):
+        c.write(data400[:1000 * (i + 1)])
+        base = ctypes.addressof(c.map)
+        assert c.content_end_pos == base + 24 + c.meta_len() + 1000 * (i + 1)
+        assert c.is_file()
+    cs[2].down()
+    assert cs[2].content_end_pos == 0
+    st.close_chunks()
+    assert st.chunks() == [] and all(c._h is None for c in cs)
+    assert sorted(os.listdir(tmp_path / "s")) == ["c0", "c1", "c2"]
+    ctx.close()
+
+
 def test_checksum_off_header(tmp_path):
     p = str(tmp_path / "nock")
     c, _ = cf.ChunkFile.open(p, flags=cf.CIO_OPEN)
