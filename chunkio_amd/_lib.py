@@ -40,7 +40,7 @@ EXPORTS = (
     "cioa_create", "cioa_destroy", "cioa_set_max_chunks_up", "cioa_set_realloc_size_hint",
     "cioa_enable_file_trimming", "cioa_disable_file_trimming", "cioa_get_flags", "cioa_set_devices",
     "cioa_last_chunk_error", "cioa_total_chunks", "cioa_total_chunks_up",
-    "cioa_stream_create", "cioa_stream_get", "cioa_stream_size_chunks_up", "cioa_stream_chunks", "cioa_scan_stream", "cioa_scan_dump",
+    "cioa_stream_create", "cioa_stream_get", "cioa_stream_size_chunks_up", "cioa_stream_chunks", "cioa_scan_stream", "cioa_scan_streams", "cioa_scan_dump",
     "cioa_chunk_open", "cioa_chunk_close", "cioa_chunk_delete", "cioa_chunk_write", "cioa_chunk_write_at",
     "cioa_chunk_sync", "cioa_chunk_sync_batch", "cioa_chunk_sync_batch_begin", "cioa_chunk_sync_batch_end",
     "cioa_chunk_get_content", "cioa_chunk_get_content_copy",

@@ -84,6 +84,7 @@ def _bind():
         "cioa_stream_chunks": (S, [V, ctypes.POINTER(V), S]),
         "cioa_stream_size_chunks_up": (S, [V]),
         "cioa_scan_stream": (V, [V, ctypes.c_char_p, ctypes.c_char_p]),
+        "cioa_scan_streams": (I, [V, ctypes.c_char_p]),
         "cioa_scan_dump": (I, [V, V]),
         "cioa_chunk_open": (V, [V, V, ctypes.c_char_p, I, S, IP]),
         "cioa_chunk_close": (None, [V, I]),
@@ -180,6 +181,18 @@ class Context:
             raise OSError(f"cannot scan stream {stream!r}")
         st = Stream(self, h, stream)
         return st, st.chunks()
+
+    def scan_all(self, ext=None):
+        """cioa_scan_streams: load every stream directory of the root (one
+        batched verify per stream): {stream name: [Chunk]}."""
+        if self._lib.cioa_scan_streams(self._h, ext.encode() if ext else None) != 0:
+            raise OSError("cannot scan the root")
+        out = {}
+        for name in sorted(os.listdir(self.root)):
+            h = self._lib.cioa_stream_get(self._h, name.encode())
+            if h:
+                out[name] = Stream(self, h, name).chunks()
+        return out
 
     def dump(self):
         """The `tools/cio -l` listing of every stream (cioa_scan_dump), as text."""

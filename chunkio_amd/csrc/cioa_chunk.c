@@ -1568,6 +1568,57 @@ cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext
     return st;
 }
 
+static int name_cmp(const void *a, const void *b)
+{
+    return strcmp(*(char *const *) a, *(char *const *) b);
+}
+
+/* cio_scan_streams (src/cio_scan.c:128-162): every directory under the root
+ * (names starting with '.' skipped) becomes a stream and is loaded with
+ * cioa_scan_stream, one verify batch per stream.  Directories in name order
+ * (the reference takes readdir order), so the max_chunks_up budget falls the
+ * same way on every filesystem.  0, or -1 when the root cannot be read. */
+int cioa_scan_streams(cioa_ctx *ctx, const char *chunk_extension)
+{
+    if (!ctx) {
+        return -1;
+    }
+    DIR *dir = opendir(ctx->root);
+    if (!dir) {
+        return -1;
+    }
+    size_t cap = 16, n = 0;
+    char **names = malloc(cap * sizeof(*names));
+    struct dirent *de;
+    while (names && (de = readdir(dir)) != NULL) {
+        if (de->d_name[0] == '.' || de->d_type != DT_DIR) {
+            continue;
+        }
+        if (n == cap) {
+            char **n2 = realloc(names, 2 * cap * sizeof(*names));
+            if (!n2) {
+                break;
+            }
+            names = n2;
+            cap *= 2;
+        }
+        if ((names[n] = strdup(de->d_name)) != NULL) {
+            n++;
+        }
+    }
+    closedir(dir);
+    if (!names) {
+        return -1;
+    }
+    qsort(names, n, sizeof(*names), name_cmp);
+    for (size_t i = 0; i < n; i++) {
+        (void) cioa_scan_stream(ctx, names[i], chunk_extension);
+        free(names[i]);
+    }
+    free(names);
+    return 0;
+}
+
 /* ---- benchmark driver (tools/cio.c:367-466) ------------------------------- */
 
 /* ---- listing (tools/cio -l) --------------------------------------------- */

@@ -27,6 +27,7 @@
  *   cioa_scan_dump                      src/cio_scan.c:171-190, cio_file.c:1316-1375 (tools/cio -l)
  *   cioa_scan_stream                    src/cio_scan.c:39-125 (verify-on-load of a stream
  *                                       directory, CIO_DELETE_IRRECOVERABLE :107-118)
+ *   cioa_scan_streams                   src/cio_scan.c:128-162 (every stream of the root)
  *
  * Where the CRC runs:
  *   - verify on open/up/scan (cio_file_format_check, cio_file.c:266-290): the
@@ -137,6 +138,10 @@ size_t cioa_stream_chunks(cioa_stream *st, cioa_chunk **out, size_t cap);
  * CIO_ERROR afterwards (cio_gpu_last_error() has the reason).  Returns the
  * stream (created if needed) or NULL. */
 cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *chunk_extension);
+/* cio_scan_streams (src/cio_scan.c:128-162, what cio_load runs): every
+ * directory under the root (names starting with '.' skipped, name order) is a
+ * stream loaded with cioa_scan_stream.  0, or -1 when the root cannot be read. */
+int cioa_scan_streams(cioa_ctx *ctx, const char *chunk_extension);
 
 /* The listing of `tools/cio -l` (cio_scan_dump, src/cio_scan.c:171-190 ->
  * cio_file_scan_dump, src/cio_file.c:1316-1375), same text, to out: per stream

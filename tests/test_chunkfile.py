@@ -549,6 +549,36 @@ def test_tx_rollback_deferred_matches_immediate(route, tmp_path, data400):
 
 
 @pytest.mark.parametrize('route', ROUTES, indirect=True)
+def test_scan_streams_loads_every_stream(route, tmp_path, data400):
+    """cioa_scan_streams (src/cio_scan.c:128-162, what cio_load runs): every
+    directory under the root is a stream loaded with one batched verify;
+    hidden directories and plain files at the root are skipped; a damaged
+    chunk is refused in its own stream only."""
+    want = {}
+    with cf.Context(str(tmp_path), cf.CIO_CHECKSUM) as ctx:
+        for si, sname in enumerate(("alpha", "beta", "gamma")):
+            st = ctx.stream(sname)
+            for i in range(4 + si):
+                c, _ = st.open(f"c{i}.flb")
+                c.write(data400[:5000 * (i + 1) + si])
+                c.sync()
+                want[(sname, f"c{i}.flb")] = c.crc_cur
+    (tmp_path / ".hidden").mkdir()
+    (tmp_path / "note.txt").write_text("not a stream")
+    with open(tmp_path / "beta" / "c1.flb", "r+b") as f:     # flip one content byte
+        f.seek(24 + 100)
+        b = f.read(1)[0]
+        f.seek(24 + 100)
+        f.write(bytes([b ^ 1]))
+    del want[("beta", "c1.flb")]
+    with cf.Context(str(tmp_path), cf.CIO_CHECKSUM, max_chunks_up=100) as ctx:
+        got = ctx.scan_all(".flb")
+        assert sorted(got) == ["alpha", "beta", "gamma"]
+        loaded = {(s, c.name): c.crc_cur for s, cs in got.items() for c in cs}
+        assert loaded == want
+
+
+@pytest.mark.parametrize('route', ROUTES, indirect=True)
 def test_scan_stream_delete_irrecoverable(route, tmp_path):
     ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM, max_chunks_up=100)
     st = ctx.stream("s")
