@@ -847,6 +847,51 @@ static void test_sync_batch_async(void)
     TEST_CHECK(diff == 0);
 }
 
+/* cioa_scan_streams over a root of three streams (cio_scan_streams,
+ * src/cio_scan.c:128-162), then cioa_chunk_close_stream on each: every chunk
+ * comes back with its crc_cur, and closing keeps the files. */
+static void test_scan_streams(void)
+{
+    int err;
+    char name[64], path[4096];
+    uint32_t crc[3][5];
+    cioa_ctx *ctx = ctx_new("streams", CIO_CHECKSUM);
+    cioa_set_max_chunks_up(ctx, 64);
+    for (int s = 0; s < 3; s++) {
+        snprintf(name, sizeof(name), "st%d", s);
+        cioa_stream *st = cioa_stream_create(ctx, name);
+        for (int i = 0; i < 5; i++) {
+            snprintf(name, sizeof(name), "c%d.flb", i);
+            cioa_chunk *c = cioa_chunk_open(ctx, st, name, CIO_OPEN, 0, &err);
+            TEST_CHECK(c != NULL);
+            cioa_chunk_write(c, in_data + s * 1000 + i, (size_t) (s * 5 + i) * 7001 + 1);
+            TEST_CHECK(cioa_chunk_sync(c) == 0);
+            crc[s][i] = cioa_chunk_crc_cur(c);
+            TEST_CHECK(cioa_chunk_is_file(c) == 1);
+            TEST_CHECK(cioa_chunk_get_content_end_pos(c) != 0);
+        }
+        cioa_chunk_close_stream(st);
+        TEST_CHECK(cioa_stream_chunks(st, NULL, 0) == 0);
+    }
+    cioa_destroy(ctx);
+    env_path(path, sizeof(path), "streams");
+    ctx = cioa_create(path, CIO_CHECKSUM | g_mode);
+    cioa_set_max_chunks_up(ctx, 64);
+    TEST_CHECK(cioa_scan_streams(ctx, ".flb") == 0);
+    for (int s = 0; s < 3; s++) {
+        snprintf(name, sizeof(name), "st%d", s);
+        cioa_stream *st = cioa_stream_get(ctx, name);
+        TEST_CHECK(st != NULL);
+        cioa_chunk *got[8];
+        TEST_CHECK(st && cioa_stream_chunks(st, got, 8) == 5);
+        for (int k = 0; st && k < 5; k++) {
+            const int i = cioa_chunk_name(got[k])[1] - '0';
+            TEST_CHECK(cioa_chunk_crc_cur(got[k]) == crc[s][i]);
+        }
+    }
+    cioa_destroy(ctx);
+}
+
 struct test {
     const char *name;
     void (*fn)(void);
@@ -874,6 +919,7 @@ static const struct test tests[] = {
     {"identity_corpus", test_identity_corpus},
     {"perf_driver", test_perf_driver},
     {"sync_batch_async", test_sync_batch_async},
+    {"scan_streams", test_scan_streams},
     {NULL, NULL},
 };
 
