@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU session ac: the final-tree checks (GPU suite, smoke, sanitizers on
+# Round-5 GPU session ac (and ag): the final-tree checks (GPU suite, smoke, sanitizers on
 # the GPU route incl. the overlapped batched sync), a cfg2 rocprofv3 pair and the
 # driver's default line.
 set -u
