@@ -2203,7 +2203,9 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
         const bool small_batch = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
         const uint64_t wmax = mx ? strtoull(mx, nullptr, 10) : small_batch ? 128 : 64;
         const uint64_t w = p->W ? ph.S / p->W : 0;
-        if (on && !oversub && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 && w % 16 == 0 &&
+        const bool any_grid = r && atoi(r) == 2;            // A/B: also on oversubscribed grids
+        if (on && (!oversub || any_grid) && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 &&
+            w % 16 == 0 &&
             w > 0 && w <= wmax) {
             const uint32_t g2 = p->grid / 32 * 31;
             PlanHost ph2;
