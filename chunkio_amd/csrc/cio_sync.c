@@ -7,6 +7,7 @@
  */
 #define _GNU_SOURCE
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -34,6 +35,12 @@ struct cio_sync_job {
     int rc;          /* prepare / run result */
     int threaded;
     pthread_t th;
+    cioa_route_plan plan;       /* engines of the CRC pass, decided before it starts */
+    /* what a threaded pass leaves in its thread's locals, handed to the
+     * caller's thread by end(): cio_gpu_last_error(), cio_gpu_pipe_last_timing() */
+    char err[512];
+    double timing[6];
+    int have_timing;
 };
 
 static void job_free(cio_sync_job *j)
@@ -85,7 +92,16 @@ static int job_prepare(cio_sync_job *j)
 static void *job_run(void *arg)
 {
     cio_sync_job *j = (cio_sync_job *) arg;
-    j->rc = cioa_crc_batch_route(j->bufs, j->lens, j->seeds, j->raw, j->m, j->ndev > 0 ? j->devs : NULL, j->ndev);
+    j->rc = cioa_crc_batch_route_planned(j->bufs, j->lens, j->seeds, j->raw, j->m, j->ndev > 0 ? j->devs : NULL,
+                                         j->ndev, &j->plan);
+    if (j->threaded) {
+        if (j->rc != CIO_OK) {
+            snprintf(j->err, sizeof(j->err), "%s", cio_gpu_last_error());
+        }
+        else if (j->plan.k > 0) {
+            j->have_timing = cio_gpu_pipe_last_timing(j->timing, 6) == CIO_OK;
+        }
+    }
     return NULL;
 }
 
@@ -142,8 +158,14 @@ static int job_start(cio_sync_item *items, size_t n, int flags, const int *devic
         j->ndev = ndev < 64 ? ndev : 64;
         memcpy(j->devs, devices, (size_t) j->ndev * sizeof(int));
     }
-    else if (async && j->m > 0 && cio_gpu_device_count() > 0) {
-        /* the job's thread runs on the caller's current device */
+    if (j->m > 0) {
+        cioa_crc_route_plan(j->lens, j->m, j->ndev > 0 ? j->devs : NULL, j->ndev, 0, &j->plan);
+    }
+    /* A pass on its own thread that will use a GPU runs on the caller's
+     * current device (a new thread starts on device 0).  A host-only pass
+     * never asks: it must not start the HIP runtime. */
+    if (async && j->m > 0 && j->plan.k > 0 && j->ndev == 0) {
+        cioa_note_hip_probe();
         const int cur = cio_gpu_get_device();
         if (cur >= 0) {
             j->devs[0] = cur;
@@ -151,15 +173,25 @@ static int job_start(cio_sync_item *items, size_t n, int flags, const int *devic
         }
     }
     if (j->m > 0) {
-        if (async && pthread_create(&j->th, NULL, job_run, j) == 0) {
-            j->threaded = 1;
-        }
-        else {
+        j->threaded = async;
+        if (!async || pthread_create(&j->th, NULL, job_run, j) != 0) {
+            j->threaded = 0;
             job_run(j);
         }
     }
     *out = j;
     return CIO_OK;
+}
+
+/* begin() with the CRC pass on the calling thread (async = 0): the chunk
+ * layer's synchronous sync goes through the same job without a thread. */
+int cioa_file_sync_batch_start(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev, int async,
+                               cio_sync_job **job)
+{
+    if (!job) {
+        return CIO_ERROR;
+    }
+    return job_start(items, n, flags, devices, ndev, async, job);
 }
 
 int cio_file_sync_batch_begin(cio_sync_item *items, size_t n, int flags, const int *devices, int ndev,
@@ -178,6 +210,12 @@ int cio_file_sync_batch_end(cio_sync_job *job)
     }
     if (job->threaded) {
         pthread_join(job->th, NULL);
+        if (job->rc != CIO_OK && job->err[0]) {
+            (void) cioa_fail_msg(job->err, NULL);
+        }
+        if (job->have_timing) {
+            cioa_pipe_timing_set(job->timing);
+        }
     }
     const int rc = job->m > 0 ? job_commit(job) : CIO_OK;
     job_free(job);

@@ -1042,7 +1042,9 @@ static void settle(cioa_chunk *ch)
     }
 }
 
-int cioa_chunk_sync_batch_begin(cioa_chunk **chunks, size_t n, cioa_sync_job **out)
+/* async: the CRC pass on a thread of its own (begin) or on this one (the
+ * synchronous sync, which then never starts a thread). */
+static int sync_batch_start(cioa_chunk **chunks, size_t n, int async, cioa_sync_job **out)
 {
     if (!out) {
         return CIO_ERROR;
@@ -1104,11 +1106,17 @@ int cioa_chunk_sync_batch_begin(cioa_chunk **chunks, size_t n, cioa_sync_job **o
     /* one pass for every deferred chunk: CRC of [crc_end, end) seeded with
      * crc_cur, on its own thread; the finalized headers and msyncs at the end */
     if (job->m > 0 &&
-        cio_file_sync_batch_begin(job->items, job->m, CIOA_SYNC_FINALIZE, ctx->devs, ctx->ndev, &job->fjob) != CIO_OK) {
+        cioa_file_sync_batch_start(job->items, job->m, CIOA_SYNC_FINALIZE, ctx->devs, ctx->ndev, async,
+                                   &job->fjob) != CIO_OK) {
         job->rc = CIO_ERROR;
     }
     *out = job;
     return CIO_OK;
+}
+
+int cioa_chunk_sync_batch_begin(cioa_chunk **chunks, size_t n, cioa_sync_job **out)
+{
+    return sync_batch_start(chunks, n, 1, out);
 }
 
 int cioa_chunk_sync_batch_end(cioa_sync_job *job)
@@ -1130,7 +1138,7 @@ int cioa_chunk_sync_batch(cioa_chunk **chunks, size_t n)
         return CIO_OK;
     }
     cioa_sync_job *job;
-    if (cioa_chunk_sync_batch_begin(chunks, n, &job) != CIO_OK) {
+    if (sync_batch_start(chunks, n, 0, &job) != CIO_OK) {
         return CIO_ERROR;
     }
     return cioa_chunk_sync_batch_end(job);

@@ -33,8 +33,30 @@ int cioa_fail_msg(const char *what, const char *detail);
  * else the GPU batch (cio_crc32_batch_host_multi / _fd_multi). */
 int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
                          size_t n, const int *devices, int ndev);
+/* Counts a query of the HIP runtime made on the route's behalf (test hook). */
+void cioa_note_hip_probe(void);
+
+/* The same in two steps: which engine(s) a batch will use (k chunks on the
+ * GPU: 0 = the host alone, n = the GPU alone, else a split), then the run.
+ * Planning never touches HIP unless a split could happen (it then checks that
+ * a GPU exists), so a caller can decide on GPU set-up before running. */
+typedef struct cioa_route_plan {
+    size_t k;
+    int gpu_bound;
+} cioa_route_plan;
+void cioa_crc_route_plan(const size_t *lens, size_t n, const int *devices, int ndev, int fd, cioa_route_plan *plan);
+int cioa_crc_batch_route_planned(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
+                                 uint32_t *out_raw, size_t n, const int *devices, int ndev,
+                                 const cioa_route_plan *plan);
 int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens, const uint32_t *seeds,
                       uint32_t *out_raw, size_t n, const int *devices, int ndev);
+
+/* cio_sync.c: cio_file_sync_batch_begin with the CRC pass on a thread of its
+ * own (async = 1) or on the calling thread (async = 0); end() as usual. */
+struct cio_sync_item;
+struct cio_sync_job;
+int cioa_file_sync_batch_start(struct cio_sync_item *items, size_t n, int flags, const int *devices, int ndev,
+                               int async, struct cio_sync_job **job);
 
 /* host_pipeline.hip: set the calling thread's cio_gpu_pipe_last_timing record
  * (6 values, as that call returns them). */

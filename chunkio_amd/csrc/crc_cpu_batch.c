@@ -154,10 +154,13 @@ static void *worker(void *arg)
         while (g_gen == seen && !g_stop) {
             pthread_cond_wait(&g_cv, &g_mu);
         }
-        if (g_stop) {
+        if (g_gen == seen) {
+            /* stopping, and no batch published since this worker's last one */
             pthread_mutex_unlock(&g_mu);
             return NULL;
         }
+        /* A published batch is served even when the stop came with it:
+         * pool_run counted this worker in g_pending and waits for it. */
         seen = g_gen;
         if (idx >= g_want) {
             continue;
@@ -188,10 +191,10 @@ __attribute__((destructor)) static void pool_stop(void)
     clock_gettime(CLOCK_REALTIME, &dl);
     dl.tv_sec += 2;
     for (int i = 0; i < n; i++) {
-        /* joined, not counted: a worker is only gone once it has returned */
-        if (pthread_timedjoin_np(g_tid[i], NULL, &dl) != 0) {
-            break;
-        }
+        /* joined, not counted: a worker is only gone once it has returned.
+         * One worker past the deadline does not stop the others from being
+         * joined (after it, each join only collects a worker already gone). */
+        (void) pthread_timedjoin_np(g_tid[i], NULL, &dl);
     }
 }
 

@@ -221,6 +221,7 @@ static const double kMaxHostOverGpu = 3.0;
 enum { kMaxT = 64 };
 static double g_rh[2][kMaxT + 1];        /* learned host rate in a split, GB/s (0: none yet) */
 static double g_rg[2];                   /* learned GPU rate per device in a split, GB/s */
+static int g_rg_seen[2];                 /* GPU parts seen per kind; the first is not learned from */
 
 int cio_crc32_split_route(void)
 {
@@ -246,21 +247,31 @@ static double ld_rate(const double *p)
     return v;
 }
 
-static void learn(double *p, double x)
+/* Running average of a rate, clamped to [model / kLearnBand, model x
+ * kLearnBand]: one outlier (a cold runtime, a host under other load) cannot
+ * push the route so far off its model that it never splits again and so never
+ * measures again. */
+static const double kLearnBand = 4.0;
+
+static void learn(double *p, double x, double model)
 {
+    const double lo = model / kLearnBand, hi = model * kLearnBand;
+    x = x < lo ? lo : x > hi ? hi : x;
     const double old = ld_rate(p);
     const double v = old > 0 ? 0.5 * old + 0.5 * x : x;
     __atomic_store(p, &v, __ATOMIC_RELAXED);
 }
 
+static double host_model(int t, int fd)
+{
+    const double m = t * (fd ? kCpuThreadFdGBps : kCpuThreadGBps);
+    return m < kCpuMemGBps ? m : kCpuMemGBps;
+}
+
 static double host_rate(int t, int fd)
 {
     const double l = ld_rate(&g_rh[fd][t]);
-    if (l > 0) {
-        return l;
-    }
-    const double m = t * (fd ? kCpuThreadFdGBps : kCpuThreadGBps);
-    return m < kCpuMemGBps ? m : kCpuMemGBps;
+    return l > 0 ? l : host_model(t, fd);
 }
 
 static double gpu_rate(int fd)
@@ -288,16 +299,33 @@ void cio_crc32_split_forget(void)
             __atomic_store(&g_rh[f][t], &z, __ATOMIC_RELAXED);
         }
         __atomic_store(&g_rg[f], &z, __ATOMIC_RELAXED);
+        __atomic_store_n(&g_rg_seen[f], 0, __ATOMIC_RELAXED);
     }
 }
 
 /* Whether a GPU is visible (checked once; a host-routed batch is only shared
  * with one that exists). */
+static int g_hip_probes;
+
+void cioa_note_hip_probe(void)
+{
+    __atomic_fetch_add(&g_hip_probes, 1, __ATOMIC_RELAXED);
+}
+
+/* Test hook (not in the public header): how often the route and the sync
+ * jobs asked the HIP runtime about devices.  A process whose batches all stay
+ * on the host must never have asked. */
+int cioa_debug_hip_probes(void)
+{
+    return __atomic_load_n(&g_hip_probes, __ATOMIC_RELAXED);
+}
+
 static int gpu_present(void)
 {
     static int v = -1;
     int x = __atomic_load_n(&v, __ATOMIC_ACQUIRE);
     if (x < 0) {
+        cioa_note_hip_probe();
         x = cio_gpu_device_count() > 0;
         __atomic_store_n(&v, x, __ATOMIC_RELEASE);
     }
@@ -314,23 +342,23 @@ static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int f
     if (mode == 0 || n < 2 || (have_max && explicit_max == 0)) {
         return gpu_bound ? n : 0;      /* (an explicit threshold of 0: the GPU alone) */
     }
-    if (!gpu_bound && !gpu_present()) {
-        return 0;                      /* host-routed, and no GPU to share with */
-    }
     if (mode != 2 && have_max && !(gpu_bound && __atomic_load_n(&g_split, __ATOMIC_ACQUIRE) == 1)) {
         /* an explicit threshold picks one engine, unless the caller also
          * turned the split on: then a batch the threshold sends to the GPU
          * may still be shared */
         return gpu_bound ? n : 0;
     }
-    const int t = cio_crc32_host_threads();
-    const double r_host = host_rate(t, fd) * 1e9;
-    const double r_gpu = (ndev_distinct > 1 ? ndev_distinct : 1) * gpu_rate(fd) * 1e9;
-    const double f = kGpuFixedUs * 1e-6;
     double total = 0;
     for (size_t i = 0; i < n; i++) {
         total += (double) lens[i];
     }
+    if (mode != 2 && total < kMinGpuShare) {
+        return gpu_bound ? n : 0;      /* no split could give the GPU its minimum share */
+    }
+    const int t = cio_crc32_host_threads();
+    const double r_host = host_rate(t, fd) * 1e9;
+    const double r_gpu = (ndev_distinct > 1 ? ndev_distinct : 1) * gpu_rate(fd) * 1e9;
+    const double f = kGpuFixedUs * 1e-6;
     if (mode != 2 && !gpu_bound && r_host >= kMaxHostOverGpu * r_gpu) {
         return 0;     /* the host alone (see kMaxHostOverGpu) */
     }
@@ -339,6 +367,11 @@ static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int f
     const double t_alone = gpu_bound ? f + total / r_gpu : total / r_host;
     if (mode != 2 && (total - b_host < kMinGpuShare || t_split >= t_alone)) {
         return gpu_bound ? n : 0;
+    }
+    /* Only now, with a split worth taking, ask whether a GPU exists: a batch
+     * the size checks keep on the host never starts the HIP runtime. */
+    if (!gpu_bound && !gpu_present()) {
+        return 0;                      /* host-routed, and no GPU to share with */
     }
     size_t k = n;
     double acc = 0;
@@ -441,11 +474,14 @@ static int run_split(const void *const *bufs, const int *fds, const uint64_t *fo
     }
     const int fd = fds != NULL;
     if (rc_host == CIO_OK && hb >= 8e6 && t_host > 0) {
-        learn(&g_rh[fd][t], hb / t_host / 1e9);
+        learn(&g_rh[fd][t], hb / t_host / 1e9, host_model(t, fd));
     }
+    /* The first GPU part of a kind also pays the runtime's, the pipeline's and
+     * the pinned buffers' set-up: it is not a rate sample. */
+    const int first_gpu = __atomic_fetch_add(&g_rg_seen[fd], 1, __ATOMIC_RELAXED) == 0;
     const double tg = g.secs - kGpuFixedUs * 1e-6;
-    if (gb >= 8e6 && tg > 0.5 * g.secs) {
-        learn(&g_rg[fd], gb / tg / 1e9 / gdev);
+    if (!first_gpu && gb >= 8e6 && tg > 0.5 * g.secs) {
+        learn(&g_rg[fd], gb / tg / 1e9 / gdev, kGpuGBps);
     }
     if (getenv("CIOA_ROUTE_DEBUG")) {
         fprintf(stderr, "split route: %zu chunks, gpu %zu (%.1f MB), host %zu (%.1f MB, %d threads): "
@@ -456,21 +492,35 @@ static int run_split(const void *const *bufs, const int *fds, const uint64_t *fo
     return rc_host;
 }
 
-int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
-                         size_t n, const int *devices, int ndev)
+void cioa_crc_route_plan(const size_t *lens, size_t n, const int *devices, int ndev, int fd, cioa_route_plan *plan)
+{
+    plan->gpu_bound = n > 0 && !route_to_cpu(lens, n, devices, ndev);
+    plan->k = n > 0 ? split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, fd, plan->gpu_bound) : 0;
+}
+
+int cioa_crc_batch_route_planned(const void *const *bufs, const size_t *lens, const uint32_t *seeds,
+                                 uint32_t *out_raw, size_t n, const int *devices, int ndev,
+                                 const cioa_route_plan *plan)
 {
     if (n == 0) {
         return CIO_OK;
     }
-    const int gpu_bound = !route_to_cpu(lens, n, devices, ndev);
-    const size_t k = split_point(lens, n, devices ? distinct_devices(devices, ndev) : 1, 0, gpu_bound);
+    const size_t k = plan->k;
     if (k == 0) {
         return cio_crc32_batch_cpu(bufs, lens, seeds, out_raw, n, cio_crc32_host_threads());
     }
     if (k < n) {
-        return run_split(bufs, NULL, NULL, lens, seeds, out_raw, n, k, devices, ndev, !gpu_bound);
+        return run_split(bufs, NULL, NULL, lens, seeds, out_raw, n, k, devices, ndev, !plan->gpu_bound);
     }
     return cio_crc32_batch_host_multi(bufs, lens, seeds, out_raw, n, devices, ndev);
+}
+
+int cioa_crc_batch_route(const void *const *bufs, const size_t *lens, const uint32_t *seeds, uint32_t *out_raw,
+                         size_t n, const int *devices, int ndev)
+{
+    cioa_route_plan plan;
+    cioa_crc_route_plan(lens, n, devices, ndev, 0, &plan);
+    return cioa_crc_batch_route_planned(bufs, lens, seeds, out_raw, n, devices, ndev, &plan);
 }
 
 int cioa_crc_fd_route(const int *fds, const uint64_t *foffs, const size_t *lens, const uint32_t *seeds,

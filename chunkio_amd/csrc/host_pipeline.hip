@@ -392,6 +392,7 @@ struct GeoKey {
 
 struct PlanImage {
     GeoKey key;
+    std::vector<uint64_t> offs, lens;   // the geometry itself (cached entries): a hit compares it whole
     std::vector<uint8_t> image;
     size_t o_desc = 0, o_ws = 0, o_tiny = 0, o_pfac = 0, o_cid = 0, npfac = 0;
     uint64_t S = 0, bytes = 0;
@@ -408,7 +409,7 @@ struct HostPipe {
     uint32_t *state = nullptr;       // running raw CRC per chunk of the call
     size_t state_cap = 0;
     std::vector<PlanImage> plans;    // plan image cache (one pipeline = one caller at a time)
-    size_t plan_bytes = 0;           // sum of the cached images
+    size_t plan_bytes = 0;           // sum of the cached images and their geometries
     uint64_t plan_clock = 0;
     GeoKey seen[kSeen];              // ring of geometries seen once (admission filter)
     int seen_next = 0;
@@ -620,8 +621,14 @@ hipError_t stage_plan(HostPipe &hp, PipeSlot &s, const HostGroup &g, DeviceState
     PlanImage *hit = nullptr;
     if (ncache) {
         key = geometry_key(g, view.W);
+        // The digest only finds a candidate; the entry's stored geometry must
+        // match in full (offsets, lengths, chunk ids), so a digest collision
+        // can never hand a group another geometry's descriptors.
         for (auto &pi : hp.plans) {
-            if (pi.key == key) {
+            if (pi.key == key && pi.offs.size() == n &&
+                memcmp(pi.offs.data(), g.offs.data(), n * sizeof(uint64_t)) == 0 &&
+                memcmp(pi.lens.data(), g.lens.data(), n * sizeof(uint64_t)) == 0 &&
+                memcmp(pi.image.data() + pi.o_cid, g.cid.data(), n * sizeof(uint32_t)) == 0) {
                 hit = &pi;
                 break;
             }
@@ -682,7 +689,7 @@ hipError_t stage_plan(HostPipe &hp, PipeSlot &s, const HostGroup &g, DeviceState
         for (const auto &k : hp.seen) {
             seen_before |= (k == key);
         }
-        const size_t sz = built.image.size();
+        const size_t sz = built.image.size() + 2 * n * sizeof(uint64_t);
         if (!seen_before) {
             hp.seen[hp.seen_next] = key;
             hp.seen_next = (hp.seen_next + 1) % kSeen;
@@ -691,12 +698,14 @@ hipError_t stage_plan(HostPipe &hp, PipeSlot &s, const HostGroup &g, DeviceState
                    (hp.plans.size() >= ncache || hp.plan_bytes + sz > plan_cache_bytes())) {
                 auto lru = std::min_element(hp.plans.begin(), hp.plans.end(),
                                             [](const PlanImage &a, const PlanImage &b) { return a.used < b.used; });
-                hp.plan_bytes -= lru->image.size();
+                hp.plan_bytes -= lru->image.size() + (lru->offs.size() + lru->lens.size()) * sizeof(uint64_t);
                 std::iter_swap(lru, hp.plans.end() - 1);
                 hp.plans.pop_back();
                 hp.evictions++;
             }
             built.key = key;
+            built.offs = g.offs;
+            built.lens = g.lens;
             hp.plan_bytes += sz;
             hp.plans.push_back(std::move(built));
             hp.stores++;

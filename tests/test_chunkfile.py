@@ -913,3 +913,75 @@ def test_split_route_learns_rates_and_matches_either_engine(cuda, tmp_path, data
         cio.split_rates(forget=True)
     key = "host_fd_t1" if threads == 1 else "host_fd_t"
     assert learned[key] != model[key] and learned["gpu_fd"] != model["gpu_fd"], (model, learned)
+
+
+def test_host_routed_syncs_never_probe_hip(tmp_path):
+    """A process whose syncs all stay on the host never asks the HIP runtime
+    about devices (the synchronous sync went through the async
+    job and looked up the current device, and the split route asked whether a
+    GPU exists before its size checks).  Fresh process, default routing (split
+    route on, one host thread): one-chunk syncs, a two-chunk batch, and a
+    begin/end batch of small deferred chunks."""
+    import subprocess
+    import sys
+    code = f"""
+import ctypes, os
+from chunkio_amd import chunkfile as cf, _lib
+lib = _lib.lib()
+lib.cioa_debug_hip_probes.restype = ctypes.c_int
+root = {str(tmp_path)!r}
+chunks = []
+for i in range(3):
+    c, _ = cf.ChunkFile.open(os.path.join(root, "s", f"c{{i}}"), deferred_crc=True)
+    c.write(b"x" * 4096)
+    chunks.append(c)
+chunks[0].sync()
+chunks[1].write(b"y" * 100)
+cf.sync_batch(chunks[:2])
+for c in chunks:
+    c.write(b"z" * 10)
+job = cf.sync_batch_begin(chunks)
+job.end()
+print("probes", lib.cioa_debug_hip_probes())
+"""
+    env = dict(os.environ)
+    for k in ("CIOA_CPU_CRC_MAX", "CIOA_SPLIT_ROUTE", "CIOA_HOST_CRC_THREADS"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    assert "probes 0" in r.stdout, r.stdout
+
+
+def test_async_sync_error_reaches_the_callers_thread(tmp_path):
+    """A begun batch whose CRC pass fails on its own thread (here: routed to
+    a GPU this process does not have, or given a device ordinal that does not
+    exist) reports the failure from end() and leaves the reason in the
+    CALLER's cio_gpu_last_error(), not only in the job thread's."""
+    import chunkio_amd as cio
+    from chunkio_amd import _lib
+    lib = cf._bind()
+    c, _ = cf.ChunkFile.open(str(tmp_path / "s" / "c0"), deferred_crc=True)
+    c.write(b"q" * 8192)
+    import ctypes
+    items = (cf.SyncItem * 1)()
+    size = ctypes.c_size_t(0)
+    m = lib.cioa_chunk_map(c._c(), ctypes.byref(size))
+    items[0].map = m
+    items[0].fs_size = size.value
+    items[0].crc_end = cf.CONTENT_OFFSET
+    items[0].crc_cur = 0xFFFFFFFF
+    items[0].data_end = 0
+    devs = (ctypes.c_int * 1)(4095)          # no such device, here or on the GPU box
+    job = ctypes.c_void_p()
+    try:
+        cio.route(reset=True, cpu_max=0)     # the GPU alone
+        _lib.lib().cio_gpu_pipe_last_timing(None, 0)   # a known, unrelated reason on this thread first
+        assert lib.cio_file_sync_batch_begin(items, 1, cf.CIOA_SYNC_FINALIZE, devs, 1, ctypes.byref(job)) == 0
+        rc = lib.cio_file_sync_batch_end(job)
+    finally:
+        cio.route(reset=True)
+        c.close()
+    assert rc != 0
+    msg = _lib.lib().cio_gpu_last_error().decode()
+    assert "null argument" not in msg and ("device" in msg or "HIP" in msg or "hip" in msg), msg
