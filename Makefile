@@ -14,12 +14,14 @@ CFLAGS   := -O3 -fPIC -Wall -Wextra -std=gnu11 $(INC)
 HIPFLAGS := -O3 -fPIC --offload-arch=$(ARCH) -std=c++17 -Wall $(INC) -munsafe-fp-atomics \
             -mllvm -amdgpu-atomic-optimizer-strategy=None -mllvm -amdgpu-kernarg-preload-count=9
 
-COBJS   := $(BLD)/host_copy.o $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o $(BLD)/cioa_chunk.o $(BLD)/crc_route.o $(BLD)/crc_cpu_batch.o
+COBJS   := $(BLD)/host_copy.o $(BLD)/crc32_host.o $(BLD)/crc32_scalar.o $(BLD)/cio_verify.o $(BLD)/cio_sync.o $(BLD)/cioa_chunk.o $(BLD)/crc_route.o $(BLD)/crc_cpu_batch.o $(BLD)/cio_sha1.o
 HOBJS   := $(BLD)/crc32_gpu.o $(BLD)/host_pipeline.o $(BLD)/sha1_gpu.o
 
 CTEST   := tests/c/bin
 REF_INC := /root/reference/include/chunkio/cio_crc32.h
-CTESTS  := $(CTEST)/test_crc32_dropin $(CTEST)/test_chunk_api $(CTEST)/test_multi $(if $(wildcard $(REF_INC)),$(CTEST)/test_crc32_dropin_ref)
+REF_SHA1 := /root/reference/src/cio_sha1.c
+CTESTS  := $(CTEST)/test_crc32_dropin $(CTEST)/test_chunk_api $(CTEST)/test_multi $(CTEST)/test_sha1 \
+           $(if $(wildcard $(REF_INC)),$(CTEST)/test_crc32_dropin_ref) $(if $(wildcard $(REF_SHA1)),$(CTEST)/test_sha1_ref)
 CLINK   := -Lchunkio_amd/lib -lchunkio_amd -Wl,-rpath,'$$ORIGIN/../../../chunkio_amd/lib'
 
 all: $(LIB) oracle ctests
@@ -36,6 +38,17 @@ $(CTEST)/test_crc32_dropin: tests/c/test_crc32_dropin.c $(LIB) include/crc32/crc
 $(CTEST)/test_crc32_dropin_ref: tests/c/test_crc32_dropin.c $(LIB) include/crc32/crc32.h
 	@mkdir -p $(CTEST)
 	$(CC) -O2 -Wall -Wextra -std=gnu11 -DCIOA_REF_BOUNDARY -Iinclude -I/root/reference/include -o $@ $< $(CLINK)
+
+# chunkio's cio_sha1 API: the library's exports, and the reference's own
+# cio_sha1.h + cio_sha1.c (unmodified, compiled where they lie) over
+# include/sha1/sha1.h -- include/ ahead of the reference's include/.
+$(CTEST)/test_sha1: tests/c/test_sha1.c $(LIB) include/sha1/sha1.h include/chunkio_amd/cio_sha1.h
+	@mkdir -p $(CTEST)
+	$(CC) -O2 -Wall -Wextra -std=gnu11 -Iinclude -o $@ $< $(CLINK)
+
+$(CTEST)/test_sha1_ref: tests/c/test_sha1.c $(REF_SHA1) $(LIB) include/sha1/sha1.h
+	@mkdir -p $(CTEST)
+	$(CC) -O2 -Wall -std=gnu11 -DCIOA_REF_BOUNDARY -Iinclude -I/root/reference/include -o $@ $< $(REF_SHA1) $(CLINK)
 
 $(CTEST)/test_chunk_api: tests/c/test_chunk_api.c $(LIB) $(wildcard include/*/*.h)
 	@mkdir -p $(CTEST)

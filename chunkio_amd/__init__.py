@@ -13,8 +13,8 @@ from .crc32 import (  # noqa: F401
     CRC_INIT, Crc32Plan, Crc32Ring, crc32, crc32_batch_cpu_packed, crc32_batch_dev, crc32_batch_host, crc32_batch_host_packed,
     crc32_combine, crc32_split_host, host_threads,
     crc32_shift, crc_finalize, crc_init, crc_update, device_count, fill_synthetic, host_register,
-    host_unregister, pipe_last_timing, plan_cache_stats, split_rates, route, sha1_batch_dev, sha1_batch_dev_async, sha1_final_batch_dev,
+    host_unregister, pipe_last_timing, plan_cache_stats, split_rates, route, Sha1, sha1_hash, sha1_to_hex, sha1_batch_dev, sha1_batch_dev_async, sha1_final_batch_dev,
     sha1_states_init, sha1_states_view, sha1_update_batch_dev,
 )
 
-__version__ = "0.4.0"
+__version__ = "0.5.0"

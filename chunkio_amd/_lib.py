@@ -32,6 +32,9 @@ EXPORTS = (
     "cio_sha1_state_init", "cio_sha1_update_batch_dev", "cio_sha1_final_batch_dev", "cio_gpu_read_stream", "cio_gpu_read_stream_grid",
     "cio_gpu_event_create", "cio_gpu_event_destroy", "cio_gpu_event_record",
     "cio_gpu_event_elapsed_ms", "cio_gpu_stream_sync",
+    # include/chunkio_amd/cio_sha1.h, include/sha1/sha1.h
+    "cio_sha1_init", "cio_sha1_update", "cio_sha1_final", "cio_sha1_hash", "cio_sha1_to_hex",
+    "cioa_SHA1_Init", "cioa_SHA1_Update", "cioa_SHA1_Final",
     # include/chunkio_amd/cio_verify.h
     "cio_file_verify_batch", "cio_file_verify_batch_multi", "cio_verify_paths", "cio_verify_paths_multi",
     # include/chunkio_amd/cio_sync.h
@@ -116,6 +119,14 @@ def _bind(lib):
         "cio_sha1_state_init": (None, [V, ctypes.c_size_t]),
         "cio_sha1_update_batch_dev": (ctypes.c_int, [V, V, V, V, ctypes.c_size_t, V]),
         "cio_sha1_final_batch_dev": (ctypes.c_int, [V, V, ctypes.c_size_t, V]),
+        "cio_sha1_init": (None, [V]),
+        "cio_sha1_update": (None, [V, V, ctypes.c_ulong]),
+        "cio_sha1_final": (None, [V, V]),
+        "cio_sha1_hash": (None, [V, ctypes.c_ulong, V, V]),
+        "cio_sha1_to_hex": (None, [V, V]),
+        "cioa_SHA1_Init": (ctypes.c_int, [V]),
+        "cioa_SHA1_Update": (ctypes.c_int, [V, V, ctypes.c_size_t]),
+        "cioa_SHA1_Final": (ctypes.c_int, [V, V]),
         "cio_gpu_read_stream": (ctypes.c_int, [V, ctypes.c_uint64, V]),
         "cio_gpu_read_stream_grid": (ctypes.c_int, [V, ctypes.c_uint64, ctypes.c_uint32, V]),
         "cio_gpu_event_create": (V, []),

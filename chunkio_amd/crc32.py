@@ -404,7 +404,60 @@ def sha1_batch_dev_async(base, dev_offs, dev_lens, dev_digests, stream=None):
                "cio_sha1_batch_dev_async")
 
 
-SHA1_STATE_BYTES = 96     # sizeof(cio_sha1_state): h[5], num, total, block[64]
+SHA1_STATE_BYTES = 96     # sizeof(cio_sha1_state) == sizeof(OpenSSL's SHA_CTX)
+
+
+class Sha1:
+    """chunkio's struct cio_sha1 (include/chunkio_amd/cio_sha1.h) on the
+    library's host SHA-1: cio_sha1_init / update / final (src/cio_sha1.c:
+    26-39).  `state` is the 96-byte SHA_CTX, OpenSSL's layout byte for byte,
+    so it can be handed to the GPU batch calls (sha1_update_batch_dev) or to
+    OpenSSL, and back."""
+
+    def __init__(self, state=None):
+        self._lib = _lib.lib()
+        self._ctx = ctypes.create_string_buffer(SHA1_STATE_BYTES)
+        if state is None:
+            self._lib.cio_sha1_init(self._ctx)
+        else:
+            state = bytes(state)
+            if len(state) != SHA1_STATE_BYTES:
+                raise ValueError(f"a SHA_CTX is {SHA1_STATE_BYTES} bytes, got {len(state)}")
+            ctypes.memmove(self._ctx, state, SHA1_STATE_BYTES)
+
+    def update(self, data):
+        b = _as_bytes(data)
+        self._lib.cio_sha1_update(self._ctx, b.ctypes.data, b.size)
+        return self
+
+    def final(self):
+        """cio_sha1_final: the 20-byte digest; the context is finished after
+        it, as OpenSSL's SHA1_Final leaves it."""
+        md = ctypes.create_string_buffer(20)
+        self._lib.cio_sha1_final(md, self._ctx)
+        return md.raw
+
+    @property
+    def state(self):
+        return self._ctx.raw
+
+
+def sha1_hash(data, want_state=False):
+    """cio_sha1_hash (src/cio_sha1.c:41-57): the digest, and with want_state
+    the 96-byte SHA_CTX as it was before SHA1_Final."""
+    b = _as_bytes(data)
+    md = ctypes.create_string_buffer(20)
+    st = ctypes.create_string_buffer(SHA1_STATE_BYTES) if want_state else None
+    _lib.lib().cio_sha1_hash(b.ctypes.data, b.size, md, st)
+    return (md.raw, st.raw) if want_state else md.raw
+
+
+def sha1_to_hex(digest):
+    """cio_sha1_to_hex (src/cio_sha1.c:59-68): 40 lowercase hex digits."""
+    d = ctypes.create_string_buffer(bytes(digest), 20)
+    out = ctypes.create_string_buffer(41)
+    _lib.lib().cio_sha1_to_hex(d, out)
+    return out.value.decode()
 
 
 def sha1_states_init(n, device):
@@ -417,11 +470,15 @@ def sha1_states_init(n, device):
 
 
 def sha1_states_view(states):
-    """Host view of device SHA-1 contexts: dict of numpy arrays h (n x 5),
-    num (n), total (n), block (n x 64)."""
-    raw = states.cpu().numpy().reshape(-1, SHA1_STATE_BYTES)
-    return {"h": raw[:, :20].copy().view("<u4"), "num": raw[:, 20:24].copy().view("<u4")[:, 0],
-            "total": raw[:, 24:32].copy().view("<u8")[:, 0], "block": raw[:, 32:].copy()}
+    """Host view of device SHA-1 contexts (SHA_CTX layout): dict of numpy
+    arrays h (n x 5), Nl, Nh, bits (Nh:Nl), num (n), data (n x 64 pending
+    bytes, zero past num), and raw (n x 96, the context bytes)."""
+    raw = states.cpu().numpy().reshape(-1, SHA1_STATE_BYTES).copy()
+    nl = raw[:, 20:24].copy().view("<u4")[:, 0]
+    nh = raw[:, 24:28].copy().view("<u4")[:, 0]
+    return {"h": raw[:, :20].copy().view("<u4"), "Nl": nl, "Nh": nh,
+            "bits": (nh.astype(np.uint64) << np.uint64(32)) | nl.astype(np.uint64),
+            "data": raw[:, 28:92].copy(), "num": raw[:, 92:96].copy().view("<u4")[:, 0], "raw": raw}
 
 
 def sha1_update_batch_dev(base, dev_offs, dev_lens, states, stream=None):

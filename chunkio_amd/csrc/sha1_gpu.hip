@@ -13,6 +13,7 @@
 // schedule runs on two more waves (sha1_kernel).
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <string.h>
 #include <string>
@@ -28,6 +29,8 @@
 #include "chunkio_amd/cio_crc32_gpu.h"
 
 static_assert(sizeof(cio_sha1_state) == 96, "cio_sha1_state is the 96-byte C ABI layout");
+static_assert(offsetof(cio_sha1_state, Nl) == 20 && offsetof(cio_sha1_state, data) == 28 &&
+              offsetof(cio_sha1_state, num) == 92, "cio_sha1_state is OpenSSL's SHA_CTX layout");
 
 namespace {
 
@@ -248,7 +251,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t len = lens[ic];
     // pending bytes of the state (kCont); the virtual message starts num bytes before p
     const uint32_t num = kCont ? (states[ic].num & 63u) : 0u;
-    const uint8_t *pend = kCont ? states[ic].block : nullptr;
+    const uint8_t *pend = kCont ? reinterpret_cast<const uint8_t *>(states[ic].data) : nullptr;
     const uint64_t vlen = len + num;
     const uint64_t full = vlen / 64;
     const uint64_t nblk = live ? (kCont ? full : full + ((len - full * 64) < 56 ? 1 : 2)) : 0;
@@ -358,7 +361,7 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     Sha1State st = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
     if (kCont && live) {
         const cio_sha1_state &s0 = states[i];
-        st = {s0.h[0], s0.h[1], s0.h[2], s0.h[3], s0.h[4]};
+        st = {s0.h0, s0.h1, s0.h2, s0.h3, s0.h4};
     }
     // Block-level pipeline: block j + 1's 20 rows are requested before block
     // j's rounds and land while they run.  The barrier that publishes group
@@ -443,20 +446,30 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         return;
     }
     if (kCont) {
-        // SHA1_Update's state: chaining value, byte count, and the tail of
-        // the virtual message as the new pending block.  The schedule waves
-        // read the old pending bytes only for block 0, before the first
-        // barrier; with no whole block there is no barrier and this wave
-        // reads them itself (tail byte k is old byte k then).
+        // SHA1_Update's state, as OpenSSL leaves its SHA_CTX: chaining
+        // value, the bit count (Nl/Nh, mod 2^64), and the tail of the virtual
+        // message as the new pending bytes, the rest of data[] zero.  The
+        // schedule waves read the old pending bytes only for block 0, before
+        // the first barrier; with no whole block there is no barrier and this
+        // wave reads them itself (tail byte k is old byte k then, read before
+        // the word holding it is written).
         cio_sha1_state &s1 = states[i];
         const uint32_t rem = (uint32_t) (vlen & 63u);
-        for (uint32_t k = 0; k < rem; ++k) {
-            const uint64_t pos = full * 64 + k;
-            s1.block[k] = pos < num ? pend[pos] : p[pos - num];
+        for (uint32_t wv = 0; wv < 16; ++wv) {
+            uint32_t word = 0;
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t k = 4 * wv + b;
+                const uint64_t pos = full * 64 + k;
+                const uint32_t byte = k < rem ? (pos < num ? pend[pos] : p[pos - num]) : 0u;
+                word |= byte << (8 * b);
+            }
+            s1.data[wv] = word;
         }
-        s1.h[0] = st.h0; s1.h[1] = st.h1; s1.h[2] = st.h2; s1.h[3] = st.h3; s1.h[4] = st.h4;
+        s1.h0 = st.h0; s1.h1 = st.h1; s1.h2 = st.h2; s1.h3 = st.h3; s1.h4 = st.h4;
+        const uint64_t bits = (((uint64_t) s1.Nh << 32) | s1.Nl) + (len << 3);
+        s1.Nl = (uint32_t) bits;
+        s1.Nh = (uint32_t) (bits >> 32);
         s1.num = rem;
-        s1.total += len;
         return;
     }
     uint8_t *out = digests + (uint64_t) i * 20;
@@ -505,15 +518,16 @@ __global__ void sha1_final_kernel(const cio_sha1_state *__restrict__ states, uin
         return;
     }
     const cio_sha1_state &s0 = states[i];
-    Sha1State st = {s0.h[0], s0.h[1], s0.h[2], s0.h[3], s0.h[4]};
+    Sha1State st = {s0.h0, s0.h1, s0.h2, s0.h3, s0.h4};
     const uint32_t num = s0.num & 63u;
-    const uint64_t bits = s0.total * 8;
+    const uint64_t bits = ((uint64_t) s0.Nh << 32) | s0.Nl;
+    const uint8_t *pend = reinterpret_cast<const uint8_t *>(s0.data);
     uint32_t w[16];
     for (int t = 0; t < 16; ++t) {
         uint32_t word = 0;
         for (int k = 0; k < 4; ++k) {
             const uint32_t pos = 4 * t + k;
-            const uint32_t byte = pos < num ? s0.block[pos] : pos == num ? 0x80u : 0u;
+            const uint32_t byte = pos < num ? pend[pos] : pos == num ? 0x80u : 0u;
             word = (word << 8) | byte;
         }
         w[t] = word;
@@ -624,13 +638,13 @@ extern "C" int cio_sha1_diag_clock(unsigned long long *out, int nwg)
 extern "C" void cio_sha1_state_init(cio_sha1_state *states, size_t n)
 {
     for (size_t k = 0; k < n; k++) {
-        cio_sha1_state &s0 = states[k];
+        cio_sha1_state &s0 = states[k];   // SHA1_Init: all zero, then H0..H4
         memset(&s0, 0, sizeof(s0));
-        s0.h[0] = 0x67452301u;
-        s0.h[1] = 0xEFCDAB89u;
-        s0.h[2] = 0x98BADCFEu;
-        s0.h[3] = 0x10325476u;
-        s0.h[4] = 0xC3D2E1F0u;
+        s0.h0 = 0x67452301u;
+        s0.h1 = 0xEFCDAB89u;
+        s0.h2 = 0x98BADCFEu;
+        s0.h3 = 0x10325476u;
+        s0.h4 = 0xC3D2E1F0u;
     }
 }
 

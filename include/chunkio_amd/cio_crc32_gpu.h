@@ -42,6 +42,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <chunkio_amd/cio_sha1_state.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -304,17 +305,13 @@ int  cio_sha1_batch_dev_async(const void *dev_base, const uint64_t *dev_offs,
 
 /* ---- SHA-1 with continuation (SHA1_Init / SHA1_Update / SHA1_Final) ----- */
 
-/* Per-chunk SHA-1 context, the state cio_sha1_init/update/final carry in an
- * SHA_CTX (src/cio_sha1.c:26-39) and cio_sha1_hash can export before its
- * SHA1_Final "for future iterations and updates" (:41-57): chaining value,
- * bytes hashed so far, and the pending partial block.  96 bytes, plain data:
+/* Per-chunk SHA-1 context: OpenSSL's SHA_CTX, byte for byte
+ * (chunkio_amd/cio_sha1_state.h) -- the context cio_sha1_init/update/final
+ * carry in struct cio_sha1 (src/cio_sha1.c:26-39) and cio_sha1_hash exports
+ * before its SHA1_Final "for future iterations and updates" (:41-57).  A
+ * context made by OpenSSL or by the host cio_sha1_* (cio_sha1.h) continues
+ * here, and one continued here continues there.  96 bytes, plain data:
  * arrays of it live in device memory for the batch calls below. */
-typedef struct cio_sha1_state {
-    uint32_t h[5];        /* chaining value H0..H4 */
-    uint32_t num;         /* bytes pending in block[] (0..63) */
-    uint64_t total;       /* message bytes hashed so far, pending ones included */
-    uint8_t  block[64];   /* pending partial block */
-} cio_sha1_state;
 
 /* SHA1_Init of n states in HOST memory (copy them to the device after). */
 void cio_sha1_state_init(cio_sha1_state *states, size_t n);

@@ -255,9 +255,16 @@ def test_continuation_random_splits(cuda):
         for i in range(n):
             pre = host[int(offs[i]):int(offs[i]) + int(b[i])].tobytes()
             assert bytes(got[i]) == hashlib.sha1(pre).digest(), (stage, i)
-            assert int(view["total"][i]) == len(pre) and int(view["num"][i]) == len(pre) % 64, (stage, i)
+            assert int(view["bits"][i]) == 8 * len(pre) and int(view["num"][i]) == len(pre) % 64, (stage, i)
             k = len(pre) % 64
-            assert view["block"][i, :k].tobytes() == pre[len(pre) - k:], (stage, i)
+            assert view["data"][i, :k].tobytes() == pre[len(pre) - k:], (stage, i)
+            assert not view["data"][i, k:].any(), (stage, i)
+            # the whole context is the host SHA-1's (pinned to OpenSSL's SHA_CTX
+            # bytes by tests/test_sha1_host.py) after the same updates
+            ref = cio.Sha1()
+            for s0 in range(stage + 1):
+                ref.update(host[int(offs[i]) + int(bounds[i, s0]):int(offs[i]) + int(bounds[i, s0 + 1])])
+            assert view["raw"][i].tobytes() == ref.state, (stage, i)
     # the full-message digests also equal the one-shot kernel's
     assert np.array_equal(cio.sha1_final_batch_dev(states), cio.sha1_batch_dev(dev, offs, lens))
 
@@ -315,3 +322,99 @@ def test_continuation_appends_cfg5_shape(cuda, golden):
     for i in (0, 511, n - 1):
         msg = host[int(offs[i]):int(offs[i] + lens[i])].tobytes() + bytes(range(1, 8))
         assert bytes(got7[i]) == hashlib.sha1(msg).digest(), i
+
+
+# ---- SHA_CTX parity with OpenSSL: contexts cross between OpenSSL and the GPU --
+
+def _openssl():
+    import ctypes
+    import ctypes.util
+    name = ctypes.util.find_library("crypto")
+    if not name:
+        pytest.skip("OpenSSL libcrypto is not installed on this box")
+    c = ctypes.CDLL(name)
+    if not all(hasattr(c, f) for f in ("SHA1_Init", "SHA1_Update", "SHA1_Final")):
+        pytest.skip("libcrypto lacks the SHA1_* API")
+    c.SHA1_Init.argtypes = [ctypes.c_void_p]
+    c.SHA1_Update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    c.SHA1_Final.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    return c
+
+
+def _ossl_ctx(c, state=None, data=b""):
+    import ctypes
+    buf = ctypes.create_string_buffer(96)
+    if state is None:
+        c.SHA1_Init(buf)
+    else:
+        ctypes.memmove(buf, bytes(state), 96)
+    if data:
+        c.SHA1_Update(buf, data, len(data))
+    return buf
+
+
+def _ossl_final(c, buf):
+    import ctypes
+    md = ctypes.create_string_buffer(20)
+    c.SHA1_Final(md, buf)
+    return md.raw
+
+
+def test_openssl_contexts_continue_on_the_gpu_and_back(cuda):
+    """Both directions, 257 chunks at random split points (padding edges
+    included), data at misaligned device offsets:
+      1. OpenSSL hashes a prefix; its 96 SHA_CTX bytes go to the device as is;
+         cio_sha1_update_batch_dev adds the middle; the device context bytes
+         equal OpenSSL's after prefix + middle;
+      2. those device bytes go back to OpenSSL, which adds the suffix and
+         finishes: the digest is the whole message's; the GPU's own final over
+         the same context (cio_sha1_final_batch_dev) agrees at the middle."""
+    import torch
+    c = _openssl()
+    rng = np.random.default_rng(81)
+    n = 257
+    edges = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 128]
+    pre_l = np.array([edges[i % len(edges)] if i < 60 else int(rng.integers(0, 5000)) for i in range(n)])
+    mid_l = np.array([edges[(i * 3) % len(edges)] if i < 60 else int(rng.integers(0, 9000)) for i in range(n)])
+    suf_l = rng.integers(0, 700, n)
+    msgs = [rng.integers(0, 256, int(a + b + s), dtype=np.uint8).tobytes() for a, b, s in zip(pre_l, mid_l, suf_l)]
+    from test_gpu_crc import pack, to_dev
+    mids = [m[int(a):int(a + b)] for m, a, b in zip(msgs, pre_l, mid_l)]
+    buf, offs, _ = pack(mids, misalign=[int(x) for x in rng.integers(0, 16, n)])
+    dev = to_dev(buf, cuda)
+    ctxs = [_ossl_ctx(c, data=m[:int(a)]) for m, a in zip(msgs, pre_l)]
+    states = torch.from_numpy(np.frombuffer(b"".join(x.raw for x in ctxs), np.uint8).copy()).to(cuda)
+    cio.sha1_update_batch_dev(dev, _dev_i64(offs, cuda), _dev_i64(mid_l, cuda), states)
+    dig_mid = cio.sha1_final_batch_dev(states)
+    raw = cio.sha1_states_view(states)["raw"]
+    for i in range(n):
+        upto = msgs[i][:int(pre_l[i] + mid_l[i])]
+        want = _ossl_ctx(c, data=upto).raw
+        assert raw[i].tobytes() == want, i
+        assert bytes(dig_mid[i]) == hashlib.sha1(upto).digest(), i
+        back = _ossl_ctx(c, state=raw[i].tobytes(), data=msgs[i][int(pre_l[i] + mid_l[i]):])
+        assert _ossl_final(c, back) == hashlib.sha1(msgs[i]).digest(), i
+
+
+def test_gpu_contexts_match_openssl_on_the_cfg5_batch(cuda):
+    """The cfg5 batch (1024 x 409,600 B) hashed on the GPU as 409,593 + 7
+    bytes per chunk: every one of the 1024 device contexts after the first
+    update equals OpenSSL's SHA_CTX after the same bytes, and OpenSSL
+    finishes each of them to the full chunk's digest."""
+    import torch
+    c = _openssl()
+    lens = wl.cfg2_lens()
+    offs = wl.packed_offsets(lens, align=16)
+    dev = torch.empty(wl.batch_bytes(offs, lens) + 64, dtype=torch.uint8, device=cuda)
+    cio.fill_synthetic(dev, offs, lens, wl.CFG2_SEED)
+    n = len(lens)
+    cut = 409593
+    states = cio.sha1_states_init(n, cuda)
+    cio.sha1_update_batch_dev(dev, _dev_i64(offs, cuda), _dev_i64(np.full(n, cut), cuda), states)
+    raw = cio.sha1_states_view(states)["raw"]
+    host = dev.cpu().numpy()
+    for i in range(n):
+        chunk = host[int(offs[i]):int(offs[i] + lens[i])].tobytes()
+        assert raw[i].tobytes() == _ossl_ctx(c, data=chunk[:cut]).raw, i
+        fin = _ossl_ctx(c, state=raw[i].tobytes(), data=chunk[cut:])
+        assert _ossl_final(c, fin) == hashlib.sha1(chunk).digest(), i
