@@ -27,6 +27,7 @@
 
 #include <sha1/sha1.h>
 #include "chunkio_amd/cio_sha1.h"
+#include "crc32_host.h"
 
 _Static_assert(sizeof(SHA_CTX) == 96, "SHA_CTX is OpenSSL's 96-byte layout");
 _Static_assert(offsetof(SHA_CTX, Nl) == 20 && offsetof(SHA_CTX, data) == 28 && offsetof(SHA_CTX, num) == 92,
@@ -166,7 +167,7 @@ static blocks_fn pick_blocks(void)
     }
     f = blocks_portable;
 #if defined(__x86_64__)
-    const char *pin = getenv("CIOA_HOST_SHA1");
+    const char *pin = cioa_diag_getenv("CIOA_HOST_SHA1");
     if (!(pin && strcmp(pin, "portable") == 0) && cpu_has_shani()) {
         f = blocks_shani;
     }

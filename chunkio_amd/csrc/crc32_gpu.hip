@@ -1956,7 +1956,7 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
 {
     p->st = st;
     p->n = (uint32_t) n;
-    if (const char *r = getenv("CIO_GPU_PRIO")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_PRIO")) {
         const int v = atoi(r);
         p->prio = (v == 0) ? 0 : 1;
     }
@@ -1967,7 +1967,7 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     // 4 KiB -3.5 %).  CIO_GPU_L64=1 / 0 forces one layout on both.
     p->l64 = true;
     p->l64_small = false;
-    if (const char *r = getenv("CIO_GPU_L64")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_L64")) {
         p->l64 = p->l64_small = atoi(r) != 0;
     }
     p->grid = (uint32_t) st->cus;
@@ -1975,7 +1975,7 @@ void plan_init(cio_crc32_plan *p, DeviceState *st, size_t n)
     // count that is not a power of two, which takes the kernels' f64 split
     // instead of the shift; more: workgroups that queue for a CU, up to 16
     // per CU).
-    if (const char *r = getenv("CIO_GPU_GRID")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_GRID")) {
         const int v = atoi(r);
         if (v >= 1 && v <= 16 * (int) p->grid) {
             p->grid = (uint32_t) v;
@@ -2120,7 +2120,7 @@ namespace {
 void plan_uniform(cio_crc32_plan *p, const uint64_t *offs, const uint64_t *lens, size_t n, const PlanHost &ph)
 {
     p->unsteps = 0;
-    if (const char *r = getenv("CIO_GPU_UNIFORM")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_UNIFORM")) {
         if (!atoi(r)) {
             return;
         }
@@ -2176,7 +2176,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // lose: 1 MiB per wave +0.8 to +5.5 %, cfg2 +5 %:
     // profiles/r04/ab_grid_oversubscribed_r04q.txt, ab_grid_cfg4_r04x.txt).
     bool oversub = false;
-    if (!getenv("CIO_GPU_GRID") && ph.S >= 1024ull * p->W && 4ull * p->W <= 65536 &&
+    if (!cioa_diag_getenv("CIO_GPU_GRID") && ph.S >= 1024ull * p->W && 4ull * p->W <= 65536 &&
         ph.S != (uint64_t) n - ph.tiny.size()) {    // (not a small-chunk batch)
         PlanHost ph4;
         if (plan_build(ph4, offs, lens, n, 4 * p->W) == nullptr) {
@@ -2197,14 +2197,14 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // +14.3 % at 16-64 chunks per wave, +3.9 % at 128.  CIO_GPU_ANTICAMP=0
     // keeps the full grid; CIO_GPU_ANTICAMP_MAX overrides the range cap.
     {
-        const char *r = getenv("CIO_GPU_ANTICAMP");
+        const char *r = cioa_diag_getenv("CIO_GPU_ANTICAMP");
         const bool on = !(r && atoi(r) == 0);
-        const char *mx = getenv("CIO_GPU_ANTICAMP_MAX");     // A/B: longest range it applies to
+        const char *mx = cioa_diag_getenv("CIO_GPU_ANTICAMP_MAX");     // A/B: longest range it applies to
         const bool small_batch = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
         const uint64_t wmax = mx ? strtoull(mx, nullptr, 10) : small_batch ? 128 : 64;
         const uint64_t w = p->W ? ph.S / p->W : 0;
         const bool any_grid = r && atoi(r) == 2;            // A/B: also on oversubscribed grids
-        if (on && (!oversub || any_grid) && !getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 &&
+        if (on && (!oversub || any_grid) && !cioa_diag_getenv("CIO_GPU_GRID") && p->grid % 32 == 0 && ph.S % p->W == 0 &&
             w % 16 == 0 &&
             w > 0 && w <= wmax) {
             const uint32_t g2 = p->grid / 32 * 31;
@@ -2227,7 +2227,7 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // it.  CIO_GPU_AHEAD=1 forces it for any uniform aligned batch, 0 never.
     p->ahead = p->unsteps != 0 && p->uh == 0 && p->uvlen % kStep == 0;
     bool short_ranges = p->S <= 64ull * p->W;
-    if (const char *r = getenv("CIO_GPU_AHEAD")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_AHEAD")) {
         short_ranges = atoi(r) != 0;
     }
     p->ahead = p->ahead && short_ranges;
@@ -2235,10 +2235,10 @@ int cio_crc32_plan_create(cio_crc32_plan **out, const uint64_t *offs, const uint
     // All chunks within one wave-step (S = number of non-tiny chunks): the
     // small-chunk kernel (CIO_GPU_SMALL=0 disables).
     p->small = ph.S > 0 && ph.S == (uint64_t) n - ph.tiny.size();
-    if (const char *r = getenv("CIO_GPU_SMALL")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_SMALL")) {
         p->small = p->small && atoi(r) != 0;
     }
-    if (const char *r = getenv("CIO_GPU_STAMPS")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_STAMPS")) {
         if (atoi(r) > 0 && hipMalloc(&p->stamps, (size_t) p->W * kStampWords * sizeof(unsigned long long)) != hipSuccess) {
             p->stamps = nullptr;
         }
@@ -2656,17 +2656,17 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
         return CIO_OK;
     }
     uint32_t B = 0;
-    if (const char *r = getenv("CIO_GPU_RS_BLOCK")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_RS_BLOCK")) {
         B = (uint32_t) atoi(r);
     }
-    if (const char *r = getenv("CIO_GPU_RS_WGPOOL")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_RS_WGPOOL")) {
         const int k = atoi(r);
         if (k > 0 && k < 65536) {
             B = 0x80000000u | (uint32_t) k;
         }
     }
     unsigned long long *stamps = nullptr;
-    if (const char *r = getenv("CIO_GPU_RS_STAMPS")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_RS_STAMPS")) {
         if (atoi(r) > 0) {
             if (!g_rs_stamps) {
                 HIP_TRY(hipMalloc(&g_rs_stamps, 65536 * 4 * sizeof(unsigned long long)), "read_stream: hipMalloc");
@@ -2676,16 +2676,16 @@ static int read_stream_impl(const void *dev_base, uint64_t bytes, void *stream, 
         }
     }
     uint32_t work = 0;
-    if (const char *r = getenv("CIO_GPU_RS_WORK")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_RS_WORK")) {
         work = (uint32_t) std::max(0, std::min(65535, atoi(r)));
     }
-    if (const char *r = getenv("CIO_GPU_RS_LANE")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_RS_LANE")) {
         // diagnostic: bytes per lane and step-row, 16 (coalesced rows), 32 or 64
         const int lb = atoi(r);
         work |= (lb == 64 ? 2u : lb == 32 ? 1u : 0u) << 16;
     }
 #if defined(CIO_DIAG_RS_DYN)
-    if (const char *r = getenv("CIO_GPU_RS_DYN")) {
+    if (const char *r = cioa_diag_getenv("CIO_GPU_RS_DYN")) {
         unsigned pm = 0, U = 4, NC = 64;
         if (sscanf(r, "%u,%u,%u", &pm, &U, &NC) >= 1 && pm > 0 && pm <= 1000 && U >= 1 && NC >= 1 &&
             NC <= 1024) {

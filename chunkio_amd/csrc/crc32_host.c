@@ -195,7 +195,7 @@ static int host_crc_mode(void)
     static int mode = -1;     /* read once; concurrent first callers compute the same value */
     int m = __atomic_load_n(&mode, __ATOMIC_RELAXED);
     if (m < 0) {
-        const char *r = getenv("CIOA_HOST_CRC");
+        const char *r = cioa_diag_getenv("CIOA_HOST_CRC");
         m = (r && strcmp(r, "table") == 0) ? 0 : (r && strcmp(r, "clmul") == 0) ? 1 : 2;
         __atomic_store_n(&mode, m, __ATOMIC_RELAXED);
     }

@@ -25,6 +25,12 @@ void cioa_stage_copy(void *dst, const void *src, size_t n);
 int cioa_stage_nt(void);            /* 1 when cioa_stage_copy uses streaming stores */
 void cioa_stage_fence(void);
 
+/* getenv(name) for a diagnostic / A/B switch (kernel choice, lane layout,
+ * grid, read-stream probes, host-path pins, staging sizes): honoured only
+ * when CIO_GPU_DIAG=1 is also set, else NULL, so a stray variable in a
+ * deployment cannot change the path.  INTEGRATION.md lists them. */
+const char *cioa_diag_getenv(const char *name);
+
 /* Record an error message for cio_gpu_last_error(); returns CIO_ERROR (-1). */
 int cioa_fail_msg(const char *what, const char *detail);
 

@@ -65,6 +65,15 @@ static const double kGpuGBps = 54.7;
 static const double kCpuThreadGBps = 36.0;
 static const double kCpuMemGBps = 131.0;
 
+const char *cioa_diag_getenv(const char *name)
+{
+    const char *gate = getenv("CIO_GPU_DIAG");
+    if (!gate || strcmp(gate, "1") != 0) {
+        return NULL;
+    }
+    return getenv(name);
+}
+
 static size_t g_cpu_max;
 static int g_cpu_max_set;
 static int g_split = -1;          /* split route: -1 not set (environment), 0 / 1 */

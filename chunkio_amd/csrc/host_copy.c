@@ -44,7 +44,7 @@ static int nt_enabled(void)
     static int v = -1;
     int x = __atomic_load_n(&v, __ATOMIC_RELAXED);
     if (x < 0) {
-        const char *r = getenv("CIO_GPU_NT_COPY");
+        const char *r = cioa_diag_getenv("CIO_GPU_NT_COPY");
         __builtin_cpu_init();
         x = (r == NULL || atoi(r) != 0) && __builtin_cpu_supports("avx2");
         __atomic_store_n(&v, x, __ATOMIC_RELAXED);

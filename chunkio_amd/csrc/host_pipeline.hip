@@ -48,7 +48,7 @@ static size_t stage_bytes()
 {
     static const size_t v = [] {
         size_t mb = 64;
-        if (const char *r = getenv("CIO_GPU_STAGE_MB")) {
+        if (const char *r = cioa_diag_getenv("CIO_GPU_STAGE_MB")) {
             const long x = atol(r);
             if (x >= 1 && x <= 1024) {
                 mb = (size_t) x;
@@ -66,7 +66,7 @@ static size_t first_stage_bytes()
 {
     static const size_t v = [] {
         size_t mb = 4;
-        if (const char *r = getenv("CIO_GPU_STAGE_FIRST_MB")) {
+        if (const char *r = cioa_diag_getenv("CIO_GPU_STAGE_FIRST_MB")) {
             const long x = atol(r);
             if (x >= 1 && x <= 1024) {
                 mb = (size_t) x;
@@ -171,7 +171,7 @@ public:
     uint64_t piece_bytes(uint64_t bytes) const
     {
         static const uint64_t fixed = [] {
-            const char *r = getenv("CIO_GPU_COPY_PIECE_KB");   // A/B knob: a fixed piece size
+            const char *r = cioa_diag_getenv("CIO_GPU_COPY_PIECE_KB");   // A/B knob: a fixed piece size
             const long v = r ? atol(r) : 0;
             return v >= 4 && v <= 65536 ? (uint64_t) v << 10 : 0;
         }();
@@ -191,7 +191,7 @@ public:
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned nw = std::min(15u, hw > 1 ? hw - 1 : 0u);
         static const bool numa = [] {
-            const char *r = getenv("CIO_GPU_COPY_NUMA");
+            const char *r = cioa_diag_getenv("CIO_GPU_COPY_NUMA");
             return !(r && r[0] == '0');
         }();
         int node = -1;
@@ -494,7 +494,7 @@ int pipes_per_dev()
 {
     static const int v = [] {
         int k = 4;
-        if (const char *r = getenv("CIO_GPU_PIPES_PER_DEV")) {
+        if (const char *r = cioa_diag_getenv("CIO_GPU_PIPES_PER_DEV")) {
             const int x = atoi(r);
             if (x >= 1 && x <= 64) {
                 k = x;

@@ -562,7 +562,7 @@ __global__ void sha1_final_kernel(const cio_sha1_state *__restrict__ states, uin
 int sha1_chunks_per_wg(size_t n)
 {
     static const int forced = [] {
-        const char *r = getenv("CIO_SHA1_CHUNKS_PER_WG");
+        const char *r = cioa_diag_getenv("CIO_SHA1_CHUNKS_PER_WG");
         const int v = r ? atoi(r) : 0;
         return (v == 8 || v == 16 || v == 32) ? v : 0;
     }();

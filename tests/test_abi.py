@@ -75,7 +75,7 @@ for n in lens:
             assert c.crc_update(s, ch) == po.crc_update(s, ch), (n, mis, s)
 print("ok")
 """
-    env = dict(os.environ, CIOA_HOST_CRC=mode)
+    env = dict(os.environ, CIOA_HOST_CRC=mode, CIO_GPU_DIAG="1")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
 
@@ -120,7 +120,7 @@ def test_crc_update_wide_crc_t_states(mode):
     import subprocess
     import sys
     code = WIDE_SEEDS_CODE.format(root=ROOT)
-    env = dict(os.environ, CIOA_HOST_CRC=mode)
+    env = dict(os.environ, CIOA_HOST_CRC=mode, CIO_GPU_DIAG="1")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stderr[-3000:]
 

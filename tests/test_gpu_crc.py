@@ -21,7 +21,9 @@ INIT = 0xFFFFFFFF
 def layout(request, monkeypatch):
     """Every test in this module runs with both lane layouts of the CRC
     kernels: L64 (one 64-byte chain per lane, permlane transpose) and the
-    4-sub-chain layout (CIO_GPU_L64 = 1 / 0, read at plan creation)."""
+    4-sub-chain layout (CIO_GPU_L64 = 1 / 0, read at plan creation).  The
+    library honours its A/B switches only under CIO_GPU_DIAG=1."""
+    monkeypatch.setenv("CIO_GPU_DIAG", "1")
     monkeypatch.setenv("CIO_GPU_L64", "1" if request.param == "l64" else "0")
     return request.param
 
@@ -476,6 +478,43 @@ def test_plan_workgroups(cuda, monkeypatch):
     monkeypatch.setenv("CIO_GPU_GRID", "17")
     with cio.Crc32Plan(wl.packed_offsets(l3), l3) as p3:
         assert p3.workgroups == 17
+
+
+def test_stray_switches_without_the_gate_change_nothing(cuda, monkeypatch):
+    """Without CIO_GPU_DIAG=1 the A/B switches are ignored: a deployment that
+    carries CIO_GPU_GRID / _SMALL / _L64 / _AHEAD / _UNIFORM / _ANTICAMP /
+    _PRIO by accident gets the shipped plans (same workgroups, same kernel)
+    and the same CRCs.  With the gate the same switches do take effect."""
+    import torch
+    knobs = {"CIO_GPU_GRID": "17", "CIO_GPU_SMALL": "0", "CIO_GPU_L64": "0", "CIO_GPU_AHEAD": "0",
+             "CIO_GPU_UNIFORM": "0", "CIO_GPU_ANTICAMP": "0", "CIO_GPU_PRIO": "0"}
+    cases = {"cfg2": wl.cfg2_lens(), "cfg4k": np.full(4096, 4096, np.uint64),
+             "camping": np.full(256 * 16 * 16, 4096, np.uint64)}
+    monkeypatch.delenv("CIO_GPU_DIAG")
+    for k in knobs:
+        monkeypatch.delenv(k, raising=False)
+    shipped = {}
+    for name, lens in cases.items():
+        offs = wl.packed_offsets(lens, align=16)
+        with cio.Crc32Plan(offs, lens) as p:
+            shipped[name] = (p.workgroups, p.kernel_name())
+    dev = torch.empty(wl.batch_bytes(wl.packed_offsets(cases["cfg4k"], align=16), cases["cfg4k"]) + 64,
+                      dtype=torch.uint8, device=cuda)
+    offs = wl.packed_offsets(cases["cfg4k"], align=16)
+    cio.fill_synthetic(dev, offs, cases["cfg4k"], 0x6A7E)
+    want = po.crc_batch(dev.cpu().numpy(), offs, cases["cfg4k"])
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    for name, lens in cases.items():
+        with cio.Crc32Plan(wl.packed_offsets(lens, align=16), lens) as p:
+            assert (p.workgroups, p.kernel_name()) == shipped[name], (name, shipped[name])
+    np.testing.assert_array_equal(cio.crc32_batch_dev(dev, offs, cases["cfg4k"]), want)
+    monkeypatch.setenv("CIO_GPU_DIAG", "1")
+    with cio.Crc32Plan(wl.packed_offsets(cases["cfg2"], align=16), cases["cfg2"]) as p:
+        assert p.workgroups == 17
+    with cio.Crc32Plan(offs, cases["cfg4k"]) as p:
+        assert p.kernel_name() != shipped["cfg4k"][1]
+    np.testing.assert_array_equal(cio.crc32_batch_dev(dev, offs, cases["cfg4k"]), want)
 
 
 @pytest.mark.parametrize("clen,per_wave,reduced", [(4096, 16, True), (4096, 128, True), (4096, 25, False),

@@ -41,6 +41,7 @@ def test_chunk_longer_than_4gib_and_offsets_past_4gib(cuda, monkeypatch):
     want = np.array([po.crc_update(int(s), host[int(o):int(o + n)]) for s, o, n in zip(seeds, offs, lens)],
                     np.uint32)
     # both lane layouts of the stream kernel
+    monkeypatch.setenv("CIO_GPU_DIAG", "1")
     for l64 in ("1", "0"):
         monkeypatch.setenv("CIO_GPU_L64", l64)
         got = cio.crc32_batch_dev(dev, offs, lens, seeds=seeds)

@@ -229,3 +229,19 @@ def test_c_callers_against_openssl(name):
         pre.update(data[off:pos])
         assert next(lines) == f"hash {md.hex()} {pre.state.hex()}"
         assert next(lines) == f"hex {md.hex()}"
+
+
+def test_path_pins_need_the_diag_gate():
+    """CIOA_HOST_SHA1=portable (an A/B pin) is ignored unless CIO_GPU_DIAG=1
+    is set too: a stray variable cannot move a deployment off the SHA
+    extensions.  (The GPU-side switches: test_gpu_crc.py's
+    test_stray_switches_without_the_gate_change_nothing.)"""
+    import sys
+    code = ("import ctypes; from chunkio_amd import _lib; l = _lib.lib(); "
+            "l.cioa_host_sha1_path.restype = ctypes.c_char_p; print(l.cioa_host_sha1_path().decode())")
+    base = {k: v for k, v in os.environ.items() if k not in ("CIO_GPU_DIAG", "CIOA_HOST_SHA1")}
+    run = lambda env: subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                                     env=env, cwd=ROOT).stdout.strip()
+    best = run(base)
+    assert run(dict(base, CIOA_HOST_SHA1="portable")) == best
+    assert run(dict(base, CIOA_HOST_SHA1="portable", CIO_GPU_DIAG="1")) == "portable"

@@ -13,6 +13,7 @@ import ctypes
 import json
 import time
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 import numpy as np

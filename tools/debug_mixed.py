@@ -5,6 +5,7 @@ several plan environments (e.g. CIO_GPU_TAIL=0 vs default), repeated launches.
     python tools/debug_mixed.py [n_chunks] [launches]
 """
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 import numpy as np

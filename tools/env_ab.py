@@ -12,6 +12,7 @@ plus the fields named by --fields (dotted paths into the bench JSON line).
 import argparse
 import json
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import subprocess
 import sys
 

@@ -94,7 +94,7 @@ grep -h -o "$REPO/include/crc32/crc32.h" "$B"/src/CMakeFiles/chunkio-static.dir/
 
 for mode in table clmul auto; do
     echo "== shim build: ctest, CIOA_HOST_CRC=$mode"
-    out=$(cd "$B" && CIOA_HOST_CRC=$mode ctest --output-on-failure 2>&1) || { echo "$out"; exit 1; }
+    out=$(cd "$B" && CIO_GPU_DIAG=1 CIOA_HOST_CRC=$mode ctest --output-on-failure 2>&1) || { echo "$out"; exit 1; }
     echo "$out" | tail -9
     check5 "$out"
 done

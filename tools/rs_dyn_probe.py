@@ -16,6 +16,7 @@ CIO_AMD_LIB=chunkio_amd/lib/ab/rsdyn.so.
 """
 import ctypes
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 import numpy as np

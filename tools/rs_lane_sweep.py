@@ -3,6 +3,7 @@
 CIO_GPU_RS_LANE=16|32|64): coalesced 1 KiB rows against 32- or 64-byte
 contiguous runs per lane, on rotating cfg2 buffers, the CRC kernel's split."""
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

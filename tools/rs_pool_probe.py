@@ -7,6 +7,7 @@ LDS atomic) against the static split, interleaved rounds in one process.
 """
 import argparse
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 import numpy as np

@@ -5,6 +5,7 @@ does the read-only kernel have the CRC kernel's spread of per-wave finish
 times, or is that spread the CRC's own?"""
 import ctypes
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 import numpy as np

@@ -3,6 +3,7 @@
 contiguous per-wave ranges (B=0) against blocks of B wave-steps dealt
 round-robin over the waves (CIO_GPU_RS_BLOCK=B), on rotating cfg2 buffers."""
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

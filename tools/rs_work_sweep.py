@@ -3,6 +3,7 @@
 and two steps in flight per wave (CIO_GPU_RS_BLOCK=0 / -1), on rotating cfg2
 buffers: how much per-step compute does each ring depth hide?"""
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -2,6 +2,7 @@
 """Per-wave phase timestamps of the CRC kernel (diagnostic build, CIO_GPU_STAMPS=1)."""
 import ctypes
 import os
+os.environ.setdefault("CIO_GPU_DIAG", "1")   # the library honours its A/B switches only with this
 import sys
 
 import numpy as np
