@@ -50,7 +50,8 @@ EXPORTS = (
     "cioa_chunk_get_content_size", "cioa_chunk_get_content_end_pos", "cioa_chunk_is_file",
     "cioa_chunk_close_stream", "cioa_chunk_get_real_size", "cioa_chunk_hash", "cioa_chunk_lock",
     "cioa_chunk_unlock", "cioa_chunk_is_locked", "cioa_chunk_tx_begin", "cioa_chunk_tx_commit",
-    "cioa_chunk_tx_rollback", "cioa_chunk_is_up", "cioa_chunk_up", "cioa_chunk_up_force", "cioa_chunk_down",
+    "cioa_chunk_tx_rollback", "cioa_chunk_is_up", "cioa_chunk_up", "cioa_chunk_up_force",
+    "cioa_chunk_up_batch", "cioa_chunk_up_force_batch", "cioa_chunk_down",
     "cioa_chunk_name", "cioa_chunk_map", "cioa_error_get", "cioa_chunk_crc_cur", "cioa_chunk_set_crc_cur",
     "cioa_meta_write", "cioa_meta_read", "cioa_meta_cmp", "cioa_meta_size", "cioa_bench_perf_write",
 )

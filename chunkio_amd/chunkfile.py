@@ -112,6 +112,8 @@ def _bind():
         "cioa_chunk_is_up": (I, [V]),
         "cioa_chunk_up": (I, [V]),
         "cioa_chunk_up_force": (I, [V]),
+        "cioa_chunk_up_batch": (I, [ctypes.POINTER(V), S, IP]),
+        "cioa_chunk_up_force_batch": (I, [ctypes.POINTER(V), S, IP]),
         "cioa_chunk_down": (I, [V]),
         "cioa_error_get": (I, [V]),
         "cioa_chunk_crc_cur": (U32, [V]),
@@ -183,8 +185,8 @@ class Context:
         return st, st.chunks()
 
     def scan_all(self, ext=None):
-        """cioa_scan_streams: load every stream directory of the root (one
-        batched verify per stream): {stream name: [Chunk]}."""
+        """cioa_scan_streams: load every stream directory of the root (the
+        verifies of all streams batched together): {stream name: [Chunk]}."""
         if self._lib.cioa_scan_streams(self._h, ext.encode() if ext else None) != 0:
             raise OSError("cannot scan the root")
         out = {}
@@ -398,6 +400,21 @@ class Chunk:
         if self._h:
             self._lib.cioa_chunk_close(self._h, 1 if delete else 0)
             self._h = None
+
+
+def up_batch(chunks, force=False):
+    """cioa_chunk_up_batch / _up_force_batch: bring the chunks up with the
+    outcome of chunk.up() / up_force() called on each in order, the verifies
+    batched.  Returns the per-chunk statuses (list of int)."""
+    if not chunks:
+        return []
+    lib = chunks[0]._lib
+    n = len(chunks)
+    arr = (ctypes.c_void_p * n)(*[c._c() for c in chunks])
+    st = (ctypes.c_int * n)()
+    fn = lib.cioa_chunk_up_force_batch if force else lib.cioa_chunk_up_batch
+    fn(arr, n, st)
+    return list(st)
 
 
 def sync_batch(chunks):

@@ -30,6 +30,15 @@
 #include "cio_layout.h"
 #include "crc32_host.h"
 
+static unsigned long g_verify_batches;
+
+/* Test hook (not in the public headers): how many non-empty verify batches
+ * ran in this process (the chunk layer's batching is checked with it). */
+unsigned long cioa_debug_verify_batches(void)
+{
+    return __atomic_load_n(&g_verify_batches, __ATOMIC_RELAXED);
+}
+
 int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags, const int *devices, int ndev)
 {
     const void **bufs = NULL;
@@ -41,6 +50,7 @@ int cio_file_verify_batch_multi(cio_verify_item *items, size_t n, int flags, con
     if (n == 0) {
         return CIO_OK;
     }
+    __atomic_fetch_add(&g_verify_batches, 1, __ATOMIC_RELAXED);
     if (!items) {
         return CIO_ERROR;
     }

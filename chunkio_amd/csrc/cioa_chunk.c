@@ -87,6 +87,7 @@ struct cioa_chunk {
     size_t tx_content_length;
     int error_n;
     struct cioa_sync_job *pending;   /* a begun, not yet ended, batch sync holding this chunk */
+    int in_round;                /* mapped and waiting in the current batched-up round */
 };
 
 static void settle(cioa_chunk *ch);
@@ -1357,31 +1358,191 @@ int cioa_chunk_tx_rollback(cioa_chunk *ch)
     return CIO_OK;
 }
 
-/* ---- up / down (cio_file.c:816-959) ----------------------------------------- */
+/* ---- up / down (cio_file.c:816-959), one chunk or a batch ----------------
+ *
+ * cio_file_up (cio_file.c:816-883): reset the chunk's error; refuse a chunk
+ * that is mapped or has an open descriptor; enforced, refuse it when
+ * total_chunks_up >= max_chunks_up (open_and_up, :564-571); open, size, map
+ * and format-check it (mmap_file: the CRC verify); on CIO_CORRUPTED or
+ * CIO_RETRY close the descriptor again.  A chunk counts as up only once its
+ * check passed (:490), so one that fails frees its slot for the next.
+ *
+ * up_rounds() runs that over a list of chunks with the outcome of calling it
+ * on each in list order, but with the CRC verifies in batches: a round opens
+ * and maps chunks while budget remains and verifies all of them in ONE routed
+ * batch (cio_file_verify_batch_multi), then the next round continues after
+ * them with the slots the failures freed.  A round also ends before a chunk
+ * of another context, with other verify flags, or already in the round (a
+ * chunk listed twice sees the first call's result, as it would in order).
+ * Scans use the same rounds over the files they register (mode UP_SCAN: past
+ * the budget a chunk is registered down, cio_file.c:566, and a chunk that
+ * fails is not registered at all, cio_scan.c:102-118). */
+
+enum { UP_ENFORCED, UP_FORCE, UP_SCAN };
+enum { UP_DOWN = 1 };            /* (scan) registered down, unverified */
+
+struct up_ent {
+    cioa_chunk *ch;
+    int ret;                     /* CIO_OK, UP_DOWN, or the CIO_* failure */
+};
+
+/* The part of cio_file_up before the CRC: checks, open, size, map.  CIO_OK
+ * with *fresh = 1: a new empty file, set up and counted by the caller. */
+static int up_prepare(cioa_chunk *ch, int mode, int *fresh)
+{
+    *fresh = 0;
+    if (mode != UP_SCAN) {
+        ch->error_n = 0;
+        if (ch->map || native_is_open(ch)) {
+            return CIO_ERROR;
+        }
+    }
+    if (native_open(ch) != CIO_OK || update_size(ch) != CIO_OK) {
+        return CIO_ERROR;
+    }
+    return map_prepare(ch, ch->fs_size, fresh);
+}
+
+static void up_failed(struct up_ent *e, int mode, int ret)
+{
+    e->ret = ret;
+    if (mode != UP_SCAN && (ret == CIO_CORRUPTED || ret == CIO_RETRY)) {
+        native_close(e->ch);
+    }
+}
+
+/* The context's last_chunk_error after entries [a, b) as calling them in
+ * order leaves it (a round records the errors of its opens before those of
+ * its verifies): an up keeps the last error any of them set; a scan resets it
+ * before every file (cio_scan.c:99), so the round's last file decides. */
+static void round_errors(const struct up_ent *e, size_t a, size_t b, int mode)
+{
+    if (a >= b) {
+        return;
+    }
+    cioa_ctx *ctx = e[a].ch->ctx;
+    if (mode == UP_SCAN) {
+        ctx->last_chunk_error = e[b - 1].ch->error_n;
+        return;
+    }
+    for (size_t k = b; k > a; k--) {
+        if (e[k - 1].ch->error_n != 0) {
+            ctx->last_chunk_error = e[k - 1].ch->error_n;
+            return;
+        }
+    }
+}
+
+static void up_rounds(struct up_ent *e, size_t n, int mode)
+{
+    cio_verify_item *items = calloc(n ? n : 1, sizeof(*items));
+    size_t *vidx = calloc(n ? n : 1, sizeof(*vidx));
+    if (!items || !vidx) {
+        for (size_t i = 0; i < n; i++) {
+            e[i].ret = mode == UP_SCAN ? UP_DOWN : CIO_ERROR;
+        }
+        free(items);
+        free(vidx);
+        return;
+    }
+    int verify_failed = 0;       /* (scan) a batch could not run: the rest are registered down */
+    size_t i = 0;
+    while (i < n) {
+        const size_t first = i;
+        cioa_ctx *ctx = e[i].ch->ctx;
+        size_t budget = ctx->max_up > ctx->total_up ? ctx->max_up - ctx->total_up : 0;
+        size_t m = 0;
+        int vflags = 0;
+        for (; i < n; i++) {
+            cioa_chunk *ch = e[i].ch;
+            const int vf = verify_flags(ch);
+            if (m > 0 && (ch->ctx != ctx || ch->in_round || vf != vflags)) {
+                break;
+            }
+            if (mode != UP_FORCE && (budget == 0 || (mode == UP_SCAN && verify_failed))) {
+                if (m > 0) {
+                    break;                   /* verify these first: failures free slots */
+                }
+                if (mode == UP_SCAN) {
+                    update_size(ch);         /* registered down */
+                    e[i].ret = UP_DOWN;
+                }
+                else {
+                    ch->error_n = 0;
+                    e[i].ret = CIO_ERROR;    /* open_and_up: over max_chunks_up */
+                }
+                continue;
+            }
+            int fresh;
+            const int ret = up_prepare(ch, mode, &fresh);
+            if (ret != CIO_OK) {
+                up_failed(&e[i], mode, ret);
+                continue;
+            }
+            if (budget > 0) {
+                budget--;
+            }
+            if (fresh) {
+                ctx->total_up++;
+                e[i].ret = CIO_OK;
+                continue;
+            }
+            items[m] = (cio_verify_item) {0};
+            items[m].map = ch->map;
+            items[m].fs_size = ch->fs_size;
+            items[m].taint = ch->taint;
+            vidx[m++] = i;
+            vflags = vf;
+            ch->in_round = 1;
+        }
+        if (m == 0) {
+            round_errors(e, first, i, mode);
+            continue;
+        }
+        const int vrc = cio_file_verify_batch_multi(items, m, vflags, ctx->devs, ctx->ndev);
+        for (size_t k = 0; k < m; k++) {
+            struct up_ent *u = &e[vidx[k]];
+            u->ch->in_round = 0;
+            if (vrc != CIO_OK) {
+                /* The batch itself could not run (GPU failure): nothing is
+                 * known about these files.  As mmap_file's CIO_ERROR, the map
+                 * goes; a scan registers them down, unverified, like the
+                 * chunks past the budget (a later up verifies them) and
+                 * reports the failure through cioa_last_chunk_error(). */
+                native_unmap(u->ch);
+                u->ch->data_size = 0;
+                if (mode == UP_SCAN) {
+                    native_close(u->ch);
+                    u->ret = UP_DOWN;
+                }
+                else {
+                    u->ret = CIO_ERROR;
+                }
+                continue;
+            }
+            const int ret = map_finish(u->ch, &items[k]);
+            if (ret != CIO_OK) {
+                up_failed(u, mode, ret);
+            }
+            else {
+                u->ret = CIO_OK;
+            }
+        }
+        round_errors(e, first, i, mode);
+        if (vrc != CIO_OK && mode == UP_SCAN) {
+            verify_failed = 1;
+            ctx->last_chunk_error = CIO_ERROR;
+        }
+    }
+    free(items);
+    free(vidx);
+}
 
 static int file_up(cioa_chunk *ch, int enforced)
 {
-    ch->error_n = 0;
-    if (ch->map) {
-        return CIO_ERROR;
-    }
-    if (native_is_open(ch)) {
-        return CIO_ERROR;
-    }
-    if (enforced && ch->ctx->total_up >= ch->ctx->max_up) {
-        return CIO_ERROR;
-    }
-    if (native_open(ch) != CIO_OK) {
-        return CIO_ERROR;
-    }
-    if (update_size(ch) != CIO_OK) {
-        return CIO_ERROR;
-    }
-    const int ret = mmap_file(ch, ch->fs_size);
-    if (ret == CIO_CORRUPTED || ret == CIO_RETRY) {
-        native_close(ch);
-    }
-    return ret;
+    struct up_ent e = {ch, CIO_ERROR};
+    up_rounds(&e, 1, enforced ? UP_ENFORCED : UP_FORCE);
+    return e.ret;
 }
 
 int cioa_chunk_up(cioa_chunk *ch)
@@ -1392,6 +1553,47 @@ int cioa_chunk_up(cioa_chunk *ch)
 int cioa_chunk_up_force(cioa_chunk *ch)
 {
     return file_up(ch, 0);
+}
+
+static int up_batch(cioa_chunk **chs, size_t n, int *status, int mode)
+{
+    if (n > 0 && !chs) {
+        return CIO_ERROR;
+    }
+    struct up_ent *e = calloc(n ? n : 1, sizeof(*e));
+    if (!e) {
+        return CIO_ERROR;
+    }
+    size_t m = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (chs[i]) {
+            e[m].ch = chs[i];
+            e[m++].ret = CIO_ERROR;
+        }
+    }
+    up_rounds(e, m, mode);
+    int rc = CIO_OK;
+    for (size_t i = 0, k = 0; i < n; i++) {
+        const int r = chs[i] ? e[k++].ret : CIO_ERROR;
+        if (status) {
+            status[i] = r;
+        }
+        if (r != CIO_OK) {
+            rc = CIO_ERROR;
+        }
+    }
+    free(e);
+    return rc;
+}
+
+int cioa_chunk_up_batch(cioa_chunk **chs, size_t n, int *status)
+{
+    return up_batch(chs, n, status, UP_ENFORCED);
+}
+
+int cioa_chunk_up_force_batch(cioa_chunk **chs, size_t n, int *status)
+{
+    return up_batch(chs, n, status, UP_FORCE);
 }
 
 int cioa_chunk_down(cioa_chunk *ch)
@@ -1410,39 +1612,34 @@ int cioa_chunk_down(cioa_chunk *ch)
     return 0;
 }
 
-/* ---- batched verify-on-load of a stream directory ----------------------- */
+/* ---- batched verify-on-load of stream directories ------------------------- */
 
-struct scan_ent {
-    char *name;
-    cioa_chunk *ch;
-    int prepared;
-};
-
-static int scan_cmp(const void *a, const void *b)
+static int name_cmp(const void *a, const void *b)
 {
-    return strcmp(((const struct scan_ent *) a)->name, ((const struct scan_ent *) b)->name);
+    return strcmp(*(char *const *) a, *(char *const *) b);
 }
 
-cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext)
+struct scan_list {
+    struct up_ent *e;
+    size_t n, cap;
+};
+
+/* Register the files of one stream directory (matching ext, name order:
+ * readdir order is filesystem-specific, name order makes the max_chunks_up
+ * budget deterministic) as new, not yet linked chunks at the end of l. */
+static int scan_collect(cioa_ctx *ctx, cioa_stream *st, const char *ext, struct scan_list *l)
 {
     char dpath[4096];
-    if (!ctx || !stream) {
-        return NULL;
-    }
-    cioa_stream *st = cioa_stream_get(ctx, stream);
-    if (!st && !(st = cioa_stream_create(ctx, stream))) {
-        return NULL;
-    }
-    snprintf(dpath, sizeof(dpath), "%s/%s", ctx->root, stream);
+    snprintf(dpath, sizeof(dpath), "%s/%s", ctx->root, st->name);
     DIR *dir = opendir(dpath);
     if (!dir) {
-        return NULL;
+        return -1;
     }
-    size_t cap = 256, n = 0;
-    struct scan_ent *ents = malloc(cap * sizeof(*ents));
+    size_t cap = 64, k = 0;
+    char **names = malloc(cap * sizeof(*names));
     const size_t ext_len = ext ? strlen(ext) : 0;
     struct dirent *de;
-    while (ents && (de = readdir(dir)) != NULL) {
+    while (names && (de = readdir(dir)) != NULL) {
         if (de->d_name[0] == '.' || de->d_type != DT_REG) {
             continue;
         }
@@ -1450,142 +1647,99 @@ cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext
         if (ext && (len <= ext_len || strncmp(de->d_name + len - ext_len, ext, ext_len) != 0)) {
             continue;
         }
-        if (n == cap) {
-            cap *= 2;
-            struct scan_ent *e2 = realloc(ents, cap * sizeof(*ents));
-            if (!e2) {
+        if (k == cap) {
+            char **n2 = realloc(names, 2 * cap * sizeof(*names));
+            if (!n2) {
                 break;
             }
-            ents = e2;
+            names = n2;
+            cap *= 2;
         }
-        if (!(ents[n].name = strdup(de->d_name))) {
-            continue;
+        if ((names[k] = strdup(de->d_name)) != NULL) {
+            k++;
         }
-        ents[n].ch = NULL;
-        ents[n].prepared = 0;
-        n++;
     }
     closedir(dir);
-    if (!ents) {
-        return NULL;
+    if (!names) {
+        return -1;
     }
-    /* readdir order is filesystem-specific; name order makes the budget of
-     * max_chunks_up deterministic */
-    qsort(ents, n, sizeof(*ents), scan_cmp);
-
-    cio_verify_item *items = calloc(n ? n : 1, sizeof(*items));
-    size_t *vidx = calloc(n ? n : 1, sizeof(*vidx));
-    /* Rounds: up to the free max_chunks_up slots are opened, mapped and then
-     * verified in one batch.  The reference counts a chunk as up only once
-     * its format check passed (cio_file.c:490), so a chunk that fails frees
-     * its slot for the next file: the next round takes the files after the
-     * batch, until the slots or the files run out.  Files past the budget are
-     * registered down, unverified (cio_file.c:566). */
-    int verify_failed = 0;
-    size_t i = 0;
-    while (i < n && items && vidx) {
-        size_t m = 0, budget = ctx->max_up > ctx->total_up ? ctx->max_up - ctx->total_up : 0;
-        int vflags = 0;
-        for (; i < n; i++) {
-            if (budget == 0 && m > 0) {
-                break;                           /* verify these first: failures free slots */
-            }
-            cioa_chunk *ch = chunk_new(ctx, st, ents[i].name, ctx->flags);
-            if (!ch) {
-                continue;
-            }
-            ents[i].ch = ch;
-            if (budget == 0 || verify_failed) {                 /* registered down */
-                update_size(ch);
-                continue;
-            }
-            int fresh = 0, ret = native_open(ch);
-            if (ret == CIO_OK && update_size(ch) != CIO_OK) {
-                ret = CIO_ERROR;
-            }
-            if (ret == CIO_OK) {
-                ret = map_prepare(ch, ch->fs_size, &fresh);
-            }
-            if (ret != CIO_OK) {
-                ents[i].prepared = ret;                         /* failed before the CRC */
-                continue;
-            }
-            budget--;
-            if (fresh) {
-                ctx->total_up++;
-                ents[i].prepared = 2;
-                continue;
-            }
-            items[m].map = ch->map;
-            items[m].fs_size = ch->fs_size;
-            items[m].taint = 0;
-            vidx[m++] = i;
-            vflags = verify_flags(ch);
-            ents[i].prepared = 1;
-        }
-        if (m == 0) {
+    qsort(names, k, sizeof(*names), name_cmp);
+    for (size_t i = 0; i < k; i++) {
+        cioa_chunk *ch = chunk_new(ctx, st, names[i], ctx->flags);
+        free(names[i]);
+        if (!ch) {
             continue;
         }
-        const int vrc = cio_file_verify_batch_multi(items, m, vflags, ctx->devs, ctx->ndev);
-        for (size_t k = 0; k < m; k++) {
-            struct scan_ent *e = &ents[vidx[k]];
-            if (vrc != CIO_OK) {
-                /* The batch itself could not run (GPU failure): nothing is
-                 * known about these files, so they are registered down,
-                 * unverified, like the chunks past the budget -- a later
-                 * cioa_chunk_up verifies them -- and the scan reports the
-                 * failure through cioa_last_chunk_error() (CIO_ERROR). */
-                native_unmap(e->ch);
-                native_close(e->ch);
-                e->ch->data_size = 0;
-                e->prepared = 0;
+        if (l->n == l->cap) {
+            const size_t c2 = l->cap ? 2 * l->cap : 256;
+            struct up_ent *e2 = realloc(l->e, c2 * sizeof(*e2));
+            if (!e2) {
+                chunk_free(ch);
                 continue;
             }
-            e->prepared = map_finish(e->ch, &items[k]) == CIO_OK ? 2 : CIO_CORRUPTED;
+            l->e = e2;
+            l->cap = c2;
         }
-        if (vrc != CIO_OK) {
-            verify_failed = 1;
-        }
+        l->e[l->n].ch = ch;
+        l->e[l->n++].ret = CIO_ERROR;
     }
-    if (verify_failed) {
-        ctx->last_chunk_error = CIO_ERROR;
-    }
-    for (size_t i = 0; i < n; i++) {
-        struct scan_ent *e = &ents[i];
-        cioa_chunk *ch = e->ch;
-        if (ch && (e->prepared == 0 || e->prepared == 2)) {
+    free(names);
+    return 0;
+}
+
+/* Load everything collected: the rounds, then link the chunks that open
+ * succeeded for (up or registered down) in order and drop the others,
+ * deleting them under CIO_DELETE_IRRECOVERABLE (cio_scan.c:107-118). */
+static void scan_load(cioa_ctx *ctx, struct scan_list *l)
+{
+    up_rounds(l->e, l->n, UP_SCAN);
+    for (size_t i = 0; i < l->n; i++) {
+        cioa_chunk *ch = l->e[i].ch;
+        const int ret = l->e[i].ret;
+        if (ret == CIO_OK || ret == UP_DOWN) {
             chunk_link(ch);
+            continue;
         }
-        else if (ch) {
-            /* cio_chunk_open failed: not registered; DELETE_IRRECOVERABLE
-             * (cio_scan.c:107-118) */
-            const int err = ch->error_n;
-            native_unmap(ch);
-            native_close(ch);
-            if ((ctx->flags & CIO_DELETE_IRRECOVERABLE) && e->prepared == CIO_CORRUPTED &&
-                (err == CIO_ERR_BAD_CHECKSUM || err == CIO_ERR_BAD_FILE_SIZE || err == CIO_ERR_BAD_LAYOUT)) {
-                (void) unlink(ch->path);
-            }
-            chunk_free(ch);
+        const int err = ch->error_n;
+        native_unmap(ch);
+        native_close(ch);
+        if ((ctx->flags & CIO_DELETE_IRRECOVERABLE) && ret == CIO_CORRUPTED &&
+            (err == CIO_ERR_BAD_CHECKSUM || err == CIO_ERR_BAD_FILE_SIZE || err == CIO_ERR_BAD_LAYOUT)) {
+            (void) unlink(ch->path);
         }
-        free(e->name);
+        chunk_free(ch);
     }
-    free(ents);
-    free(items);
-    free(vidx);
+    free(l->e);
+    l->e = NULL;
+    l->n = l->cap = 0;
+}
+
+cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *ext)
+{
+    if (!ctx || !stream) {
+        return NULL;
+    }
+    cioa_stream *st = cioa_stream_get(ctx, stream);
+    if (!st && !(st = cioa_stream_create(ctx, stream))) {
+        return NULL;
+    }
+    struct scan_list l = {0};
+    if (scan_collect(ctx, st, ext, &l) != 0) {
+        free(l.e);
+        return NULL;
+    }
+    scan_load(ctx, &l);
     return st;
 }
 
-static int name_cmp(const void *a, const void *b)
-{
-    return strcmp(*(char *const *) a, *(char *const *) b);
-}
-
 /* cio_scan_streams (src/cio_scan.c:128-162): every directory under the root
- * (names starting with '.' skipped) becomes a stream and is loaded with
- * cioa_scan_stream, one verify batch per stream.  Directories in name order
- * (the reference takes readdir order), so the max_chunks_up budget falls the
- * same way on every filesystem.  0, or -1 when the root cannot be read. */
+ * (names starting with '.' skipped) becomes a stream, and all of their files
+ * load through ONE set of rounds: directories in name order (the reference
+ * takes readdir order), files in name order within each, the max_chunks_up
+ * budget falling on that order -- the result of loading the streams one after
+ * the other -- with each round's verifies in one batch across streams, so a
+ * root of many small streams still fills a GPU batch.  0, or -1 when the root
+ * cannot be read. */
 int cioa_scan_streams(cioa_ctx *ctx, const char *chunk_extension)
 {
     if (!ctx) {
@@ -1619,11 +1773,16 @@ int cioa_scan_streams(cioa_ctx *ctx, const char *chunk_extension)
         return -1;
     }
     qsort(names, n, sizeof(*names), name_cmp);
+    struct scan_list l = {0};
     for (size_t i = 0; i < n; i++) {
-        (void) cioa_scan_stream(ctx, names[i], chunk_extension);
+        cioa_stream *st = cioa_stream_get(ctx, names[i]);
+        if (st || (st = cioa_stream_create(ctx, names[i]))) {
+            (void) scan_collect(ctx, st, chunk_extension, &l);
+        }
         free(names[i]);
     }
     free(names);
+    scan_load(ctx, &l);
     return 0;
 }
 

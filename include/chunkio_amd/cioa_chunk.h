@@ -23,6 +23,7 @@
  *   cioa_chunk_lock / _unlock / _is_locked             src/cio_chunk.c:384-416
  *   cioa_chunk_tx_begin / _commit / _rollback          src/cio_chunk.c:423-502
  *   cioa_chunk_is_up / _up / _up_force / _down         src/cio_chunk.c:509-605, cio_file.c:816-959
+ *   cioa_chunk_up_batch / _up_force_batch  the same up over many chunks, verifies batched
  *   cioa_meta_write / _read / _cmp / _size             src/cio_meta.c:46-180, cio_file.c:1075-1145
  *   cioa_scan_dump                      src/cio_scan.c:171-190, cio_file.c:1316-1375 (tools/cio -l)
  *   cioa_scan_stream                    src/cio_scan.c:39-125 (verify-on-load of a stream
@@ -33,7 +34,8 @@
  *   - verify on open/up/scan (cio_file_format_check, cio_file.c:266-290): the
  *     batched verify (cio_file_verify_batch_multi, routed by crc_route.c to
  *     the GPU or, for small batches, the host crc_update); cioa_scan_stream
- *     verifies every chunk it maps in ONE batch;
+ *     and cioa_scan_streams verify every chunk they map in ONE batch (across
+ *     streams), and cioa_chunk_up_batch the chunks it brings up;
  *   - the per-write update (update_checksum, cio_file.c:97-113): crc_update
  *     on the caller's buffer, as the reference does -- unless the context
  *     has CIOA_DEFERRED_CRC, where writes only copy and the CRC of every
@@ -140,7 +142,10 @@ size_t cioa_stream_chunks(cioa_stream *st, cioa_chunk **out, size_t cap);
 cioa_stream *cioa_scan_stream(cioa_ctx *ctx, const char *stream, const char *chunk_extension);
 /* cio_scan_streams (src/cio_scan.c:128-162, what cio_load runs): every
  * directory under the root (names starting with '.' skipped, name order) is a
- * stream loaded with cioa_scan_stream.  0, or -1 when the root cannot be read. */
+ * stream loaded as cioa_scan_stream loads one, with the same result as
+ * loading them one after the other -- but every stream's files go through
+ * one set of rounds, so a round's verify batch spans streams (a root of many
+ * small streams fills one GPU batch).  0, or -1 when the root cannot be read. */
 int cioa_scan_streams(cioa_ctx *ctx, const char *chunk_extension);
 
 /* The listing of `tools/cio -l` (cio_scan_dump, src/cio_scan.c:171-190 ->
@@ -197,6 +202,16 @@ int  cioa_chunk_tx_rollback(cioa_chunk *ch);
 int  cioa_chunk_is_up(cioa_chunk *ch);
 int  cioa_chunk_up(cioa_chunk *ch);
 int  cioa_chunk_up_force(cioa_chunk *ch);
+/* cio_chunk_up / cio_chunk_up_force (src/cio_chunk.c:573-605 -> cio_file_up,
+ * cio_file.c:816-883) over n chunks with the outcome of n calls in list
+ * order -- per-chunk status[i] (CIO_OK / CIO_ERROR / CIO_CORRUPTED /
+ * CIO_RETRY, may be NULL), error numbers, crc_cur, the max_chunks_up budget
+ * (enforced: a chunk that fails its check frees its slot for the next) --
+ * with the CRC verifies of the chunks brought up in as few routed batches as
+ * that order allows (one, unless failures free slots, or the list mixes
+ * contexts or open modes).  Returns CIO_OK when every chunk came up. */
+int  cioa_chunk_up_batch(cioa_chunk **chunks, size_t n, int *status);
+int  cioa_chunk_up_force_batch(cioa_chunk **chunks, size_t n, int *status);
 int  cioa_chunk_down(cioa_chunk *ch);
 const char *cioa_chunk_name(cioa_chunk *ch);
 /* The chunk's mapping (NULL when down) and its mapped size (cf->map,

@@ -592,7 +592,9 @@ def test_scan_stream_delete_irrecoverable(route, tmp_path):
     ctx = cf.Context(str(tmp_path), cf.CIO_CHECKSUM | cf.CIO_DELETE_IRRECOVERABLE, max_chunks_up=100)
     st, chunks = ctx.scan("s")
     assert [c.name for c in chunks] == [f"c{i:02d}" for i in range(20) if i != 5]
-    assert ctx.last_chunk_error == cf.CIO_ERR_BAD_CHECKSUM
+    # the scan resets last_chunk_error before every file (cio_scan.c:99): after
+    # the last file (c19, loaded) it is 0 again
+    assert ctx.last_chunk_error == 0
     assert all(c.is_up() for c in chunks)
     assert [c.data_size for c in chunks] == [1000 * i + 1 for i in range(20) if i != 5]
     ctx.close()
@@ -732,7 +734,8 @@ def test_scan_budget_counts_only_loaded_chunks(route, tmp_path):
     assert [(c.name, c.is_up()) for c in chunks] == [("c00", True), ("c02", True), ("c03", True),
                                                        ("c04", False), ("c05", False)]
     assert ctx.total_chunks_up == 3
-    assert ctx.last_chunk_error == cf.CIO_ERR_BAD_CHECKSUM
+    # reset before every file (cio_scan.c:99): the last file, c05, registered down
+    assert ctx.last_chunk_error == 0
     assert [c.data_size for c in chunks if c.is_up()] == [3, 1403, 2103]
     ctx.close()
     assert not (tmp_path / "s" / "c01").exists()

@@ -1,0 +1,237 @@
+"""Batched up and cross-stream scans (cioa_chunk_up_batch, cioa_scan_streams).
+
+Reference: cio_chunk_up / cio_chunk_up_force (src/cio_chunk.c:573-605) ->
+cio_file_up (src/cio_file.c:816-883): each call resets the chunk's error,
+refuses a mapped chunk or one with an open descriptor, enforces
+max_chunks_up (open_and_up, :564-571; default 64, include/chunkio/chunkio.h:63),
+then maps and format-checks the file (the CRC verify) and counts it up only
+if that passed (:490).  cio_scan_streams (src/cio_scan.c:128-162) loads the
+streams one after the other.
+
+The oracle here is the library's own one-at-a-time path, which the reference
+fixtures and the C replays of the reference's tests pin (test_ref_chunks.py,
+test_c_api.py): n sequential cioa_chunk_up calls on one copy of the files,
+one cioa_chunk_up_batch on another, and every per-chunk outcome (status, error
+number, crc_cur, up/down, content size), the context's counters and the files
+themselves must agree -- with the verifies in a few batches instead of one per
+chunk.  The reference-written fixtures (tests/golden/chunks/) are also brought
+up in a batch against the reference loader's own verdicts.  Host route in the
+CPU suite; GPU and split routes under -m gpu.
+"""
+import ctypes
+import json
+import os
+import shutil
+
+import pytest
+
+from chunkio_amd import _lib
+from chunkio_amd import chunkfile as cf
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GDIR = os.path.join(HERE, "golden", "chunks")
+
+ROUTES = [pytest.param("host", id="host"), pytest.param("gpu", marks=pytest.mark.gpu, id="gpu"),
+          pytest.param("split", marks=pytest.mark.gpu, id="split")]
+
+
+@pytest.fixture
+def route(request):
+    import chunkio_amd as cio
+    if request.param == "gpu":
+        request.getfixturevalue("cuda")
+        cio.route(reset=True, cpu_max=0)
+    elif request.param == "split":
+        request.getfixturevalue("cuda")
+        cio.route(reset=True, cpu_max=1, threads=1, split="force")
+    else:
+        cio.route(reset=True, cpu_max=1 << 62, threads=1)
+    yield request.param
+    cio.route(reset=True)
+
+
+def verify_batches():
+    lib = _lib.lib()
+    lib.cioa_debug_verify_batches.restype = ctypes.c_ulong
+    return int(lib.cioa_debug_verify_batches())
+
+
+def _damage(path, kind):
+    size = os.path.getsize(path)
+    with open(path, "r+b") as f:
+        if kind == "crc":                 # a content bit: BAD_CHECKSUM
+            f.seek(size - 5)
+            b = f.read(1)[0] ^ 0x10
+            f.seek(size - 5)
+            f.write(bytes([b]))
+        elif kind == "magic":             # BAD_LAYOUT
+            f.write(b"\x00\x00")
+        elif kind == "short":             # content length past the end: BAD_FILE_SIZE
+            f.truncate(30)
+        elif kind == "empty":             # a 0-byte file: set up fresh on open
+            f.truncate(0)
+
+
+def make_stream(root, stream, n, damage, seed=0):
+    """n checksummed chunk files stream/c000.. with 3..40 KB of content each;
+    damage: {index: kind}."""
+    d = os.path.join(root, stream)
+    for i in range(n):
+        c, _ = cf.ChunkFile.open(os.path.join(d, f"c{i:03d}"))
+        c.write(bytes(((i * 7 + k + seed) % 251) for k in range(3000 + (i * 977) % 37000)))
+        c.sync()
+        c.close()
+    for i, kind in damage.items():
+        _damage(os.path.join(d, f"c{i:03d}"), kind)
+    return d
+
+
+def snapshot(root):
+    out = {}
+    for dp, _, files in os.walk(root):
+        for f in files:
+            p = os.path.join(dp, f)
+            out[os.path.relpath(p, root)] = open(p, "rb").read()
+    return out
+
+
+def outcome(c, ret):
+    return (ret, c.error, c.is_up(), c.crc_cur if c.is_up() else None, c.data_size if c.is_up() else None)
+
+
+DAMAGE = {3: "crc", 10: "magic", 40: "short", 63: "crc", 64: "crc", 70: "empty", 150: "crc"}
+
+
+def _down_everything(ctx, stream):
+    _, chunks = ctx.scan(stream)
+    for c in chunks:
+        if c.is_up():
+            assert c.down() == 0
+    return chunks
+
+
+@pytest.mark.parametrize("route", ROUTES, indirect=True)
+@pytest.mark.parametrize("force", [False, True], ids=["up", "up_force"])
+def test_up_batch_equals_sequential_up(route, tmp_path, force):
+    """200 chunks registered down, max_chunks_up 64, damaged chunks inside and
+    past the first 64 (bad checksum, bad magic, truncated, a 0-byte file), one
+    chunk already up and one listed twice: cioa_chunk_up_batch gives each
+    chunk what cioa_chunk_up gives it in list order, and the files end equal."""
+    roots = []
+    for tag in ("seq", "bat"):
+        root = str(tmp_path / tag)
+        make_stream(root, "s", 200, DAMAGE)
+        roots.append(root)
+    results, counters, batches = [], [], []
+    for k, root in enumerate(roots):
+        with cf.Context(root, cf.CIO_CHECKSUM | cf.CIO_OPEN, max_chunks_up=64) as ctx:
+            chunks = _down_everything(ctx, "s")
+            assert ctx.total_chunks_up == 0
+            assert chunks[0].up() == cf.CIO_OK           # already up when the list runs
+            order = chunks[::-1][:120] + chunks[:90] + [chunks[17]]
+            b0 = verify_batches()
+            if k == 0:
+                rets = [c.up_force() if force else c.up() for c in order]
+            else:
+                rets = cf.up_batch(order, force=force)
+            batches.append(verify_batches() - b0)
+            results.append([outcome(c, r) for c, r in zip(order, rets)])
+            counters.append((ctx.total_chunks_up, ctx.last_chunk_error))
+    assert results[0] == results[1]
+    assert counters[0] == counters[1]
+    assert snapshot(roots[0]) == snapshot(roots[1])
+    ups = sum(1 for r in results[1] if r[0] == cf.CIO_OK)
+    assert ups >= 63 and batches[0] >= ups - 2          # one verify per chunk, one at a time
+    assert batches[1] <= 8, batches                     # a handful of rounds
+
+
+@pytest.mark.parametrize("route", ROUTES, indirect=True)
+def test_up_batch_one_round_and_budget(route, tmp_path):
+    """Undamaged chunks: one verify batch brings up exactly the budget's
+    worth in list order; the rest get CIO_ERROR (open_and_up) with error 0."""
+    root = str(tmp_path / "r")
+    make_stream(root, "s", 100, {})
+    with cf.Context(root, cf.CIO_CHECKSUM, max_chunks_up=64) as ctx:
+        chunks = _down_everything(ctx, "s")
+        b0 = verify_batches()
+        rets = cf.up_batch(chunks)
+        assert verify_batches() - b0 == 1
+        assert rets == [cf.CIO_OK] * 64 + [cf.CIO_ERROR] * 36
+        assert [c.is_up() for c in chunks] == [True] * 64 + [False] * 36
+        assert all(c.error == 0 for c in chunks)
+        assert ctx.total_chunks_up == 64
+        assert cf.up_batch([]) == []
+
+
+@pytest.mark.parametrize("route", ROUTES, indirect=True)
+def test_up_batch_reference_fixtures(route, tmp_path):
+    """The 14 chunk files the reference wrote and damaged
+    (tests/golden/chunks/), registered down and brought up in one batched up:
+    a chunk the reference loader loaded comes up with its crc_cur and content
+    size; one it refused is refused with its error number, as a one-by-one up
+    does."""
+    with open(os.path.join(GDIR, "manifest.json")) as f:
+        man = json.load(f)
+    by = {s["name"]: s for s in man["chunks"]}
+    names = [n for n in sorted(by) if by[n]["load_flags"] & cf.CIO_CHECKSUM]
+    outs = []
+    for tag in ("seq", "bat"):
+        d = tmp_path / tag / man["stream"]
+        d.mkdir(parents=True)
+        for n in names:
+            shutil.copyfile(os.path.join(GDIR, "files", n), d / n)
+        with cf.Context(str(tmp_path / tag), cf.CIO_CHECKSUM, max_chunks_up=1) as ctx:
+            _, chunks = ctx.scan(man["stream"])         # the first loads, the rest register down
+            for c in chunks:
+                if c.is_up():
+                    c.down()
+            ctx._lib.cioa_set_max_chunks_up(ctx._h, 64)
+            rets = [c.up() for c in chunks] if tag == "seq" else cf.up_batch(chunks)
+            outs.append({c.name: outcome(c, r) for c, r in zip(chunks, rets)})
+    assert outs[0] == outs[1]
+    got = outs[1]
+    assert set(got) == set(names)
+    for n, (ret, err, up, crc, size) in got.items():
+        ld = by[n]["load"]
+        if ld["ok"]:
+            assert (ret, up, crc, size) == (cf.CIO_OK, True, ld["crc_cur"], ld["content_size"]), n
+        else:
+            assert ret != cf.CIO_OK and not up and err == ld["last_chunk_error"], (n, ret, err, ld)
+
+
+@pytest.mark.parametrize("route", ROUTES, indirect=True)
+@pytest.mark.parametrize("delete", [False, True], ids=["keep", "delete_irrecoverable"])
+def test_scan_streams_batches_across_streams(route, tmp_path, delete):
+    """Six streams of 25 files with damage in several, max_chunks_up 64:
+    cioa_scan_streams loads exactly what scanning the streams one after the
+    other in name order loads (chunks, up/down, crc_cur, sizes, deleted files
+    under CIO_DELETE_IRRECOVERABLE, counters), in far fewer verify batches."""
+    flags = cf.CIO_CHECKSUM | (cf.CIO_DELETE_IRRECOVERABLE if delete else 0)
+    dmg = {"s0": {2: "crc"}, "s1": {}, "s2": {0: "magic", 24: "short"}, "s3": {5: "crc", 6: "crc"},
+           "s4": {}, "s5": {1: "empty", 24: "crc"}}
+    roots = []
+    for tag in ("seq", "all"):
+        root = str(tmp_path / tag)
+        for k, (st, dm) in enumerate(dmg.items()):
+            make_stream(root, st, 25, dm, seed=k)
+        roots.append(root)
+    views, batches = [], []
+    for k, root in enumerate(roots):
+        with cf.Context(root, flags, max_chunks_up=64) as ctx:
+            b0 = verify_batches()
+            if k == 0:
+                got = {st: ctx.scan(st)[1] for st in sorted(dmg)}
+            else:
+                got = ctx.scan_all()
+            batches.append(verify_batches() - b0)
+            views.append(({st: [(c.name, c.is_up(), c.crc_cur if c.is_up() else None,
+                                 c.data_size if c.is_up() else None) for c in chunks]
+                           for st, chunks in got.items()}, ctx.total_chunks_up, ctx.last_chunk_error))
+    assert views[0] == views[1]
+    assert snapshot(roots[0]) == snapshot(roots[1])
+    assert views[1][1] == 64
+    # past the budget the last file is registered down unverified: the scan
+    # leaves last_chunk_error 0, as the reference's reset before each file does
+    assert views[1][2] == 0
+    assert batches[1] < batches[0], batches
+    assert batches[1] <= 3, batches
