@@ -38,6 +38,12 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+try:
+    # the process's CPUs before any leg binds it to its GPU's NUMA node
+    # (bind_to_gpu_node); the all-devices leg runs on all of them again
+    ORIG_AFFINITY = os.sched_getaffinity(0)
+except AttributeError:
+    ORIG_AFFINITY = None
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -50,7 +56,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=200)
-    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e", "perf", "verify"])
+    p.add_argument("--config", default="cfg2",
+                   choices=["cfg2", "cfg3", "cfg4", "cfg4k", "sha1", "e2e", "perf", "verify", "multi"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--no-extra", action="store_true",
                    help="cfg2 only: skip the 4 KiB (cfg4k) and 4 MiB (cfg4) lines reported in 'other_chunk_sizes'")
@@ -1159,6 +1166,29 @@ def run_perf(args, rank, world, device, dist, compact=False):
                              "crc_off_GBps": ref["crc_off"]["GBps"], **cpu_info()}}
 
 
+def make_perf_files(root, files=1000, bad=500):
+    """The 1000 chunk files `tools/cio -k -p` leaves (2,068,480 B each: header,
+    5 x 400kb.txt, CRC 0x088740E7), written once through the chunk layer and
+    copied, with a flipped content byte in file `bad`."""
+    import shutil
+    from chunkio_amd import chunkfile as cf
+    d400 = np.fromfile(os.path.join(ROOT, "tests", "golden", "400kb.txt"), dtype=np.uint8).tobytes()
+    paths = [os.path.join(root, f"perf-test-{i:04d}.txt") for i in range(files)]
+    c, _ = cf.ChunkFile.open(paths[0], deferred_crc=True)
+    for _ in range(5):
+        c.write(d400)
+    cf.sync_batch([c])
+    c.close()
+    for p in paths[1:]:
+        shutil.copyfile(paths[0], p)
+    with open(paths[bad], "r+b") as f:
+        f.seek(24 + 123456)
+        b = f.read(1)
+        f.seek(24 + 123456)
+        f.write(bytes([b[0] ^ 0x20]))
+    return paths
+
+
 def run_verify(args, rank, world, device, dist, compact=False):
     """batched verify-on-load of a stream directory.  1000
     chunk files as `tools/cio -k -p` leaves them (2,068,480 B each: header,
@@ -1177,19 +1207,7 @@ def run_verify(args, rank, world, device, dist, compact=False):
     ncpu = 100 if compact else 200
     root = tempfile.mkdtemp(prefix="cioa-verify-")
     try:
-        paths = [os.path.join(root, f"perf-test-{i:04d}.txt") for i in range(files)]
-        c, _ = cf.ChunkFile.open(paths[0], deferred_crc=True)
-        for _ in range(5):
-            c.write(d400)
-        cf.sync_batch([c])
-        c.close()
-        for p in paths[1:]:
-            shutil.copyfile(paths[0], p)
-        with open(paths[bad], "r+b") as f:
-            f.seek(24 + 123456)
-            b = f.read(1)
-            f.seek(24 + 123456)
-            f.write(bytes([b[0] ^ 0x20]))
+        paths = make_perf_files(root, files, bad)
         fsize = os.path.getsize(paths[0])
         region = 2 + 5 * len(d400)              # [22, 24 + meta_len + content_len)
         for _ in range(max(1, args.warmup)):
@@ -1273,6 +1291,159 @@ def run_verify(args, rank, world, device, dist, compact=False):
            "check": check}
     if cpu is not None:
         res["cpu_baseline"] = cpu
+    return res
+
+
+def multi_device_list(world, visible, rehearse):
+    """Device entries for the all-devices leg: 0..N-1, or -- rehearsing N
+    ranks on fewer GPUs -- the visible ones round-robin (shared: True).
+    None when the GPUs are too few and this is not a rehearsal."""
+    if visible >= world:
+        return list(range(world)), False
+    if not rehearse or visible < 1:
+        return None, True
+    return [i % visible for i in range(world)], True
+
+
+def node_cpus(node):
+    """CPUs of a NUMA node (sysfs cpulist), empty when unknown."""
+    cpus = set()
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+    except (OSError, ValueError):
+        pass
+    return cpus
+
+
+def _multi_device_host(args, world, device):
+    """Rank 0's half of multi_device_host_leg (see there)."""
+    import hashlib
+    import shutil
+    import torch
+    import chunkio_amd as cio
+    from chunkio_amd import chunkfile as cf
+    from chunkio_amd import workloads as wl
+    rehearse = os.environ.get("CIO_BENCH_REHEARSE") == "1"
+    devices, shared = multi_device_list(world, torch.cuda.device_count(), rehearse)
+    if devices is None:
+        return {"error": f"{world} devices wanted, {torch.cuda.device_count()} visible"}
+    if ORIG_AFFINITY:
+        os.sched_setaffinity(0, ORIG_AFFINITY)       # undo the per-GPU NUMA binding of the e2e leg
+    res = {"devices": devices, "shared_devices_rehearsal": shared}
+    # -- (1) the weak cfg2 job of N GPUs (N x 1024 x 409,600 B) in pageable host
+    #    memory, one cio_crc32_batch_host_multi call: chunk k -> devices[k % N]
+    n = wl.CFG2_N * world
+    lens = np.full(n, wl.CFG2_LEN, dtype=np.uint64)
+    offs = wl.packed_offsets(lens, align=16)
+    total = int(lens.sum())
+    gen = torch.empty(wl.batch_bytes(offs, lens) + 16, dtype=torch.uint8, device=device)
+    cio.fill_synthetic(gen, offs, lens, wl.CFG2_SEED, ids=np.arange(n, dtype=np.uint64))
+    host = gen.cpu().numpy()
+    del gen
+    torch.cuda.empty_cache()
+    out = cio.crc32_batch_host_packed(host, offs, lens, devices=devices)        # warm: pipelines, pools
+    reps = max(1, min(args.steps, 5))
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = cio.crc32_batch_host_packed(host, offs, lens, devices=devices)
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    want = weak_job_golden("cfg2", world)
+    per_dev = {}
+    for k, d in enumerate(devices):
+        per_dev.setdefault(str(d), 0)
+        per_dev[str(d)] += int(lens[k::len(devices)].sum())
+    numa = {}
+    for d in sorted(set(devices)):
+        node = int(cio.lib().cio_gpu_numa_node(d))
+        local = node_cpus(node) & (ORIG_AFFINITY or set()) if node >= 0 else set()
+        numa[str(d)] = {"numa_node": node, "node_cpus_in_affinity": len(local),
+                        "copy_threads": min(15, max(0, (os.cpu_count() or 1) - 1)) + 1,   # CopyPool + caller
+                        "copy_threads_pinned_to_node": bool(local)}
+    host_cpu = {}
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nproc = os.cpu_count() or 1
+    for tn in sorted({16, min(64, nproc)}):
+        cio.crc32_batch_cpu_packed(host, offs, lens, threads=tn)
+        tt = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            got = cio.crc32_batch_cpu_packed(host, offs, lens, threads=tn)
+            tt.append(time.perf_counter() - t0)
+        host_cpu[f"threads_{tn}"] = {"GBps": round(total / min(tt) / 1e9, 2), "ms": round(min(tt) * 1e3, 3),
+                                     "equals_gpu": bool(np.array_equal(got, out))}
+    host_cpu["note"] = (f"cio_crc32_batch_cpu over the same host batch (16 threads, and this process's CPUs "
+                        f"up to the pool's 64: {nproc} in affinity)")
+    res["host_batch_multi"] = {
+        "call": "cio_crc32_batch_host_multi (staged: copy pools -> pinned staging -> H2D -> kernel, "
+                "every device's pipeline concurrently)",
+        "GBps": round(total / t / 1e9, 3), "ms": round(t * 1e3, 3), "bytes": total, "chunks": n,
+        "per_device_GBps": round(total / t / 1e9 / len(set(devices)), 3),
+        "bytes_per_device": per_dev, "numa_per_device": numa, "reps": reps,
+        "check": {"golden_sha256_match_full_job": (hashlib.sha256(np.asarray(out, dtype="<u4").tobytes())
+                                                   .hexdigest() == want) if want else None},
+        "host_cpu_batch": host_cpu}
+    del host
+    # -- (2) verify-on-load of the 1000 perf files with devices[] (file ranges
+    #    pread by each device's copy pool; cio_verify_paths_multi)
+    root = tempfile.mkdtemp(prefix="cioa-multi-")
+    try:
+        files, bad = 1000, 500
+        paths = make_perf_files(root, files, bad)
+        region = 2 + 5 * 409600
+        ok_idx = [i for i in range(files) if i != bad]
+        legs = {}
+        nt = host_cpu_threads()
+        try:
+            for tag, kw in (("gpus_alone", {"cpu_max": 0}), ("default_route", {}),
+                            (f"host_threads_{nt}", {"cpu_max": -1, "threads": nt})):
+                cio.route(reset=True, **kw)
+                cf.verify_paths(paths, devices=devices)
+                vt = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    st, er, cr = cf.verify_paths(paths, devices=devices)
+                    vt.append(time.perf_counter() - t0)
+                legs[tag] = {"GBps": round(files * region / min(vt) / 1e9, 3), "ms": round(min(vt) * 1e3, 3),
+                             "check": bool(np.all(st[ok_idx] == 0)
+                                           and np.all((cr[ok_idx] ^ 0xFFFFFFFF) == 0x088740E7)
+                                           and st[bad] == -3 and er[bad] == -10)}
+        finally:
+            cio.route(reset=True)
+        legs["note"] = ("one cio_verify_paths_multi call over 1000 x 2,068,480-B files in the page cache; "
+                        "gpus_alone: every CRC byte on the devices (threshold 0); default_route: the "
+                        "route as shipped (one host CRC thread, split route on); host_threads_N: every "
+                        "batch on N host threads, no GPU")
+        res["verify_paths_multi"] = legs
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return res
+
+
+def multi_device_host_leg(args, rank, world, device, dist, runner=None):
+    """How ONE chunkio process would use every GPU of the node for chunks in
+    host memory (Fluent Bit is one process: src/cio_scan.c:39-125 loads every
+    stream in it): after the per-rank legs, rank 0 alone -- the other ranks
+    wait at a barrier -- calls the library's single-process multi-device API
+    with devices = 0..N-1: cio_crc32_batch_host_multi over the whole weak cfg2
+    job of N GPUs (N x 1024 x 409,600 B, checked against its reference digest)
+    and cio_verify_paths_multi over the 1000 perf files; beside them the host's
+    own CRC over the same batch on 16 threads and on the process's CPUs.  At
+    N = 1 it is the e2e and verify legs again on device 0.  Returns rank 0's
+    result (None on the other ranks)."""
+    barrier(dist)
+    res = None
+    if rank == 0:
+        t0 = time.perf_counter()
+        res = (runner or _multi_device_host)(args, world, device)
+        res["wall_s"] = round(time.perf_counter() - t0, 2)
+    barrier(dist)
     return res
 
 
@@ -1539,6 +1710,14 @@ def main():
         res = run_perf(args, rank, world, device, dist)
     elif args.config == "verify":
         res = run_verify(args, rank, world, device, dist)
+    elif args.config == "multi":
+        multi = multi_device_host_leg(args, rank, world, device, dist)
+        res = {"metric": "single-process all-devices host-memory CRC32 GB/s (cio_crc32_batch_host_multi)",
+               "value": multi["host_batch_multi"]["GBps"] if multi else None, "unit": "GB/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "u8", "data": "synthetic, pageable host memory",
+               "config": {"workload": "weak cfg2 job of N GPUs from one process, devices 0..N-1"},
+               "multi_device_host": multi}
     else:
         res = run_crc(args, rank, world, device, dist)
         if args.config == "cfg2" and not args.no_extra:
@@ -1548,6 +1727,9 @@ def main():
             # SDMA engines the H2D copies use, which slows host batches by
             # ~11% for ~1 s after such a free (profiles/r04/e2e_vram_free/README.md).
             host_legs = other_configs(args, rank, world, device, dist, only=("e2e", "verify", "perf"))
+            multi = multi_device_host_leg(args, rank, world, device, dist)
+            if multi is not None:
+                res["multi_device_host"] = multi
             res["other_chunk_sizes"] = other_chunk_sizes(args, rank, world, device, dist)
             dev_legs = other_configs(args, rank, world, device, dist, only=("cfg3", "sha1"))
             wall = host_legs.pop("wall_s") + dev_legs.pop("wall_s")

@@ -424,3 +424,55 @@ def test_bench_cpu_baselines_at_n2():
     bad = dig.copy()
     bad[3, 0] ^= 1
     assert not bench.sha1_cpu_baseline(host, offs, lens, bad, world=2)["bit_exact_vs_gpu"]
+
+
+def _multi_leg_worker(rank, world, port, q):
+    import os
+    import time
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def runner(args, w, device):
+            calls.append(w)
+            time.sleep(0.5)                 # the others must wait for rank 0 here
+            return {"devices": bench.multi_device_list(w, 1, True)[0]}
+        t0 = time.perf_counter()
+        res = bench.multi_device_host_leg(None, rank, world, "cpu", dist, runner=runner)
+        q.put((rank, res, calls, time.perf_counter() - t0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_multi_device_leg_rank0_alone_gloo_world2():
+    """bench.py's all-devices host leg at world size 2 on gloo: rank 0 alone
+    runs the single-process multi-device calls (a stub here: no GPU on this
+    side) while rank 1 waits at the leg's barriers, and only rank 0's line
+    carries the result; the device list is 0..N-1, or the visible GPUs
+    round-robin in a rehearsal, and refused otherwise."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multi_leg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        rank, res, calls, dt = q.get(timeout=120)
+        out[rank] = (res, calls, dt)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert out[0][1] == [2] and out[1][1] == []
+    assert out[0][0]["devices"] == [0, 0] and "wall_s" in out[0][0]
+    assert out[1][0] is None
+    assert out[1][2] >= 0.45                # rank 1 was held until rank 0 finished
+    import bench
+    assert bench.multi_device_list(8, 8, False) == (list(range(8)), False)
+    assert bench.multi_device_list(2, 1, True) == ([0, 0], True)
+    assert bench.multi_device_list(4, 2, True) == ([0, 1, 0, 1], True)
+    assert bench.multi_device_list(2, 1, False) == (None, True)
+    assert bench.multi_device_list(1, 1, False) == ([0], False)
