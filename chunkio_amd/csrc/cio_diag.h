@@ -101,11 +101,35 @@
 #ifndef CIO_SHA1_CHAINS
 #define CIO_SHA1_CHAINS 32
 #endif
+/* A/B: the round wave issues the next block's 20 row reads after this many
+ * rows (x 4 rounds) of the current block; 0 = before it (shipped). */
+#ifndef CIO_SHA1_READ_AT
+#define CIO_SHA1_READ_AT 0
+#endif
+/* A/B: blocks per barrier of the 8-chunk geometry (cfg5's). */
+#ifndef CIO_SHA1_GROUP8
+#define CIO_SHA1_GROUP8 8
+#endif
 
 /* A/B: 1 drops the asm anchor that keeps each block's rounds ahead of the
  * next block's row reads (correct results, slower). */
 #ifndef CIO_SHA1_NO_ANCHOR
 #define CIO_SHA1_NO_ANCHOR 0
+#endif
+
+/* Timing-only ablations of the SHA-1 kernel (WRONG digests on purpose; A/B
+ * builds for tools/sha1_ab.py --diag, profiles/r06/sha1_attribution/):
+ * NOREAD: the round wave reads two blocks' rows once and reuses them (no LDS
+ * row reads in the loop); NOBAR: no hand-over barriers; NOSCHED: the schedule
+ * wave exits at once (use with NOBAR). */
+#ifndef CIO_SHA1_DIAG_NOREAD
+#define CIO_SHA1_DIAG_NOREAD 0
+#endif
+#ifndef CIO_SHA1_DIAG_NOBAR
+#define CIO_SHA1_DIAG_NOBAR 0
+#endif
+#ifndef CIO_SHA1_DIAG_NOSCHED
+#define CIO_SHA1_DIAG_NOSCHED 0
 #endif
 
 /* Diagnostic: per-workgroup shader-clock records of the round loop, read back

@@ -494,7 +494,7 @@ int pipes_per_dev()
 {
     static const int v = [] {
         int k = 4;
-        if (const char *r = cioa_diag_getenv("CIO_GPU_PIPES_PER_DEV")) {
+        if (const char *r = getenv("CIO_GPU_PIPES_PER_DEV")) {
             const int x = atoi(r);
             if (x >= 1 && x <= 64) {
                 k = x;

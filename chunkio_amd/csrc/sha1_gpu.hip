@@ -141,11 +141,17 @@ __device__ __forceinline__ void cont_block(const uint8_t *p, const uint8_t *pend
 
 // The 80 rounds of one block from its K_t + W_t rows, folded into the chaining
 // value: 5 VALU per round (two rotates, v_bitop3 round function, add, add3).
-__device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20])
+// mid() runs after row kMidRow's rounds (A/B CIO_SHA1_READ_AT: where the next
+// block's row reads are issued; 0 = before the block, the shipped order).
+template <int kMidRow = 0, class Mid>
+__device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20], Mid &&mid)
 {
     uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
 #pragma unroll
     for (int r = 0; r < 20; ++r) {
+        if (kMidRow > 0 && r == kMidRow) {
+            mid();
+        }
         const uint32_t kwv[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -160,6 +166,11 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
         }
     }
     st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
+}
+
+__device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20])
+{
+    sha1_block_rounds<0>(st, rows, [] {});
 }
 
 // One workgroup = one round wave + kShaSched schedule waves for the same
@@ -201,6 +212,17 @@ static_assert(kShaPer % 2 == 0, "the round wave's rows alternate between two reg
 // 8 chunks/WG with 8 blocks per barrier 4.813 ms, 16/8 4.822, 16/4 4.831,
 // 32/4 4.862; profiles/r03/sha1/ab_sha1_chains_r03zu.txt), but a round wave
 // then does 64/C times the work per chain, so larger batches keep 32.
+// The hand-over barrier between the schedule wave and the round wave.
+// Timing-only diagnostic builds (cio_diag.h CIO_SHA1_DIAG_*: wrong digests on
+// purpose, tools/sha1_ab.py --diag) drop it, the round wave's row reads, or
+// the schedule wave, to attribute the kernel's time to each.
+__device__ __forceinline__ void sha1_barrier()
+{
+#if !CIO_SHA1_DIAG_NOBAR
+    __syncthreads();
+#endif
+}
+
 template <int C, int P>
 struct ShaGeom {
     static constexpr int kChains = C;
@@ -214,7 +236,7 @@ struct ShaGeom {
 };
 using ShaGeomWide = ShaGeom<kShaChains, kShaPer>;   // the default (CIO_SHA1_CHAINS / GROUP for A/B)
 using ShaGeom16 = ShaGeom<16, 8>;
-using ShaGeom8 = ShaGeom<8, 8>;
+using ShaGeom8 = ShaGeom<8, CIO_SHA1_GROUP8>;
 
 #if CIO_SHA1_CLOCK_DIAG
 // Diagnostic builds only: per workgroup, the round wave's shader-clock and
@@ -265,6 +287,9 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     }
     const uint64_t ngroups = (wmax + kShaPer - 1) / kShaPer;
 
+    if (sched && CIO_SHA1_DIAG_NOSCHED) {
+        return;                 // timing-only: no message schedule, the round wave alone
+    }
     if (sched) {
         // Aligned content blocks come from a kShaAhead-deep register ring
         // (this lane's block j + kShaAhead kShaStreams is requested when block
@@ -349,12 +374,12 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                 if (jb + (uint64_t) u * kShaStreams < ngroups * kShaPer) {
                     produce(jb + sw + (uint64_t) u * kShaStreams, nx[u]);
                     if ((u * kShaStreams) % kShaPer == kShaPer - kShaStreams) {
-                        __syncthreads();
+                        sha1_barrier();
                     }
                 }
             }
         }
-        __syncthreads();
+        sha1_barrier();
         return;
     }
 
@@ -380,13 +405,13 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     // still runs the rounds (the wave issues them anyway) and a lane past its
     // last block keeps its state through a select (a per-lane branch measured
     // 5% slower in round 2: the compiler then spilled rows).
-    auto run_block = [&](auto kAll, uint64_t jb, const uint4 (&rows)[kShaRowsPerBlock]) {
+    auto run_block = [&](auto kAll, uint64_t jb, const uint4 (&rows)[kShaRowsPerBlock], auto &&mid) {
         if (decltype(kAll)::value) {
-            sha1_block_rounds(st, rows);
+            sha1_block_rounds<CIO_SHA1_READ_AT>(st, rows, mid);
             return;
         }
         Sha1State nxs = st;
-        sha1_block_rounds(nxs, rows);
+        sha1_block_rounds<CIO_SHA1_READ_AT>(nxs, rows, mid);
         const bool take = jb < nblk;
         st.h0 = take ? nxs.h0 : st.h0; st.h1 = take ? nxs.h1 : st.h1; st.h2 = take ? nxs.h2 : st.h2;
         st.h3 = take ? nxs.h3 : st.h3; st.h4 = take ? nxs.h4 : st.h4;
@@ -409,14 +434,24 @@ sha1_kernel(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             // (more than lgkmcnt's 4-bit count can wait past).
             __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
             if (u == kShaPer - 1) {
-                __syncthreads();
+                sha1_barrier();
             }
-            load_block(jb + 1, (u & 1) ? ra : rb);   // after the last group: read, not used
-            __builtin_amdgcn_sched_barrier(0);       // the next block's reads go out before the rounds
-            run_block(kAll, jb, (u & 1) ? rb : ra);
+            auto next_rows = [&] {
+#if !CIO_SHA1_DIAG_NOREAD
+                load_block(jb + 1, (u & 1) ? ra : rb);   // after the last group: read, not used
+#endif
+                __builtin_amdgcn_sched_barrier(0);       // the next block's reads go out here
+            };
+            if (CIO_SHA1_READ_AT == 0) {
+                next_rows();
+            }
+            run_block(kAll, jb, (u & 1) ? rb : ra, next_rows);
         }
     };
-    __syncthreads();
+    sha1_barrier();
+#if CIO_SHA1_DIAG_NOREAD
+    load_block(0, rb);          // both register sets read once; every block reuses them
+#endif
 #if CIO_SHA1_CLOCK_DIAG
     const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();

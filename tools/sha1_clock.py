@@ -48,7 +48,9 @@ def main():
         ln = np.ascontiguousarray(np.tile(lens0, copies).astype(np.uint64))
         n = len(ln)
         out = torch.empty(n * 20, dtype=torch.uint8, device="cuda")
-        nwg = (n + 31) // 32
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        per = 8 if n <= 8 * cus else 16 if n <= 16 * cus else 32     # sha1_chunks_per_wg's geometry
+        nwg = (n + per - 1) // per
         rows = []
         for it in range(args.iters):
             t0 = time.perf_counter()
