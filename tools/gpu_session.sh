@@ -48,7 +48,7 @@ for step in "$@"; do
     prof)
       IFS=: read -r cfg steps warm args <<< "$rest"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_${cfg}_$n" -o run --output-format csv -- \
-          python3 bench.py --config "$cfg" --steps "${steps:-300}" --warmup "${warm:-200}" --no-cpu ${args//+/ } \
+          python3 bench.py --config "$cfg" --steps "${steps:-300}" --warmup "${warm:-200}" --no-cpu --no-extra ${args//+/ } \
           > "$O/bench_prof_${cfg}_$n.json" 2> "$O/prof_${cfg}_$n.err"
       stop_if_failed $? "prof $cfg" ;;
     pmc)
