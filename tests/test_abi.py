@@ -20,10 +20,10 @@ def declared_functions():
     names = set()
     for hdr in ("include/crc32/crc32.h", "include/chunkio_amd/cio_crc32_gpu.h",
                 "include/chunkio_amd/cio_verify.h", "include/chunkio_amd/cio_sync.h",
-                "include/chunkio_amd/cioa_chunk.h"):
+                "include/chunkio_amd/cioa_chunk.h", "include/chunkio_amd/cio_sha1.h", "include/sha1/sha1.h"):
         text = open(os.path.join(ROOT, hdr)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-        for m in re.finditer(r"^\s*(?!static|typedef|#)[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(",
+        for m in re.finditer(r"^\s*(?!static|typedef|#)[A-Za-z_][\w\s\*]*?\b([a-z_][A-Za-z0-9_]*)\s*\(",
                              text, flags=re.M):
             names.add(m.group(1))
     return names
@@ -33,6 +33,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     decl = declared_functions()
     assert "crc_update" in decl and "cio_crc32_plan_exec" in decl
+    assert {"cio_sha1_hash", "cioa_SHA1_Update", "cioa_chunk_up_batch"} <= decl
     missing = [n for n in sorted(decl) if not hasattr(lib, n)]
     assert not missing, missing
     assert set(_lib.EXPORTS) >= decl, sorted(decl - set(_lib.EXPORTS))
