@@ -1456,8 +1456,8 @@ static void up_rounds(struct up_ent *e, size_t n, int mode)
         for (; i < n; i++) {
             cioa_chunk *ch = e[i].ch;
             const int vf = verify_flags(ch);
-            if (m > 0 && (ch->ctx != ctx || ch->in_round || vf != vflags)) {
-                break;
+            if (ch->ctx != ctx || (m > 0 && (ch->in_round || vf != vflags))) {
+                break;                       /* (a round's budget and devices are its context's) */
             }
             if (mode != UP_FORCE && (budget == 0 || (mode == UP_SCAN && verify_failed))) {
                 if (m > 0) {

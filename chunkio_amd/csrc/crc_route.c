@@ -267,7 +267,7 @@ static void learn(double *p, double x, double model)
     const double lo = model / kLearnBand, hi = model * kLearnBand;
     x = x < lo ? lo : x > hi ? hi : x;
     const double old = ld_rate(p);
-    const double v = old > 0 ? 0.5 * old + 0.5 * x : x;
+    double v = old > 0 ? 0.5 * old + 0.5 * x : x;
     __atomic_store(p, &v, __ATOMIC_RELAXED);
 }
 
@@ -302,7 +302,7 @@ void cio_crc32_split_rates(double *out, int n)
 
 void cio_crc32_split_forget(void)
 {
-    const double z = 0;
+    double z = 0;
     for (int f = 0; f < 2; f++) {
         for (int t = 0; t <= kMaxT; t++) {
             __atomic_store(&g_rh[f][t], &z, __ATOMIC_RELAXED);

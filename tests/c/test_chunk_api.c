@@ -892,6 +892,108 @@ static void test_scan_streams(void)
     cioa_destroy(ctx);
 }
 
+/* ---- batched up (cioa_chunk_up_batch) ------------------------------------ */
+
+/* n chunk files in <sub>/s, content of varied sizes; chunk k with k % 7 == 3
+ * gets a flipped content byte on disk (BAD_CHECKSUM at its next verify). */
+static void ub_build(const char *sub, int n, int seed)
+{
+    int err;
+    char name[64];
+    cioa_ctx *ctx = ctx_new(sub, CIO_CHECKSUM);
+    cioa_stream *st = cioa_stream_create(ctx, "s");
+    for (int i = 0; i < n; i++) {
+        snprintf(name, sizeof(name), "c%03d", i);
+        cioa_chunk *c = cioa_chunk_open(ctx, st, name, CIO_OPEN, 0, &err);
+        TEST_CHECK(c != NULL);
+        cioa_chunk_write(c, in_data + (seed * 131 + i) % 4096, (size_t) 1000 + (size_t) ((i * 7919 + seed) % 60000));
+        TEST_CHECK(cioa_chunk_sync(c) == 0);
+    }
+    cioa_destroy(ctx);
+    for (int i = 3; i < n; i += 7) {
+        char path[4096];
+        snprintf(name, sizeof(name), "%s/s/c%03d", sub, i);
+        env_path(path, sizeof(path), name);
+        int fd = open(path, O_RDWR);
+        unsigned char b = 0;
+        TEST_CHECK(fd >= 0 && pread(fd, &b, 1, 30) == 1);
+        b ^= 0x40;
+        TEST_CHECK(pwrite(fd, &b, 1, 30) == 1);
+        close(fd);
+    }
+}
+
+/* Open <sub> with max_chunks_up = max, scan, put every chunk down: *out
+ * holds the stream's chunks (registered, all down). */
+static cioa_ctx *ub_load_down(const char *sub, int max, cioa_chunk **out, size_t cap, size_t *n)
+{
+    char path[4096];
+    env_path(path, sizeof(path), sub);
+    cioa_ctx *ctx = cioa_create(path, CIO_CHECKSUM | g_mode);
+    cioa_set_max_chunks_up(ctx, max);
+    cioa_stream *st = cioa_scan_stream(ctx, "s", NULL);
+    TEST_CHECK(st != NULL);
+    *n = st ? cioa_stream_chunks(st, out, cap) : 0;
+    for (size_t k = 0; k < *n && k < cap; k++) {
+        if (cioa_chunk_is_up(out[k])) {
+            cioa_chunk_down(out[k]);
+        }
+    }
+    return ctx;
+}
+
+/* cioa_chunk_up_batch over chunks of two contexts interleaved (budgets 8 and
+ * 5, damaged chunks among them, one chunk listed twice) against the same
+ * cioa_chunk_up calls in order on copies of the files: every status, error
+ * number, crc_cur and up state, and both contexts' counters, agree. */
+static void test_up_batch(void)
+{
+    cioa_chunk *a[2][64], *b[2][64], *list[2][140];
+    size_t na[2], nb[2], m[2] = {0, 0};
+    int st[2][140];
+    ub_build("ubA0", 40, 1);
+    ub_build("ubB0", 30, 2);
+    ub_build("ubA1", 40, 1);
+    ub_build("ubB1", 30, 2);
+    cioa_ctx *ca[2], *cb[2];
+    for (int r = 0; r < 2; r++) {
+        ca[r] = ub_load_down(r ? "ubA1" : "ubA0", 8, a[r], 64, &na[r]);
+        cb[r] = ub_load_down(r ? "ubB1" : "ubB0", 5, b[r], 64, &nb[r]);
+        /* scans dropped the damaged chunks they reached; the rest are down */
+        for (size_t k = 0; k < na[r] || k < nb[r]; k++) {
+            if (k < na[r]) list[r][m[r]++] = a[r][k];
+            if (k < nb[r]) list[r][m[r]++] = b[r][k];
+        }
+        list[r][m[r]++] = a[r][2];
+    }
+    TEST_CHECK(m[0] == m[1] && na[0] > 20 && nb[0] > 15);
+    for (size_t k = 0; k < m[0]; k++) {
+        st[0][k] = cioa_chunk_up(list[0][k]);
+    }
+    TEST_CHECK(cioa_chunk_up_batch(list[1], m[1], st[1]) == CIO_ERROR);   /* not all came up */
+    int diff = 0, up = 0;
+    for (size_t k = 0; k < m[0]; k++) {
+        const int u0 = cioa_chunk_is_up(list[0][k]), u1 = cioa_chunk_is_up(list[1][k]);
+        if (st[0][k] != st[1][k] || u0 != u1 || cioa_error_get(list[0][k]) != cioa_error_get(list[1][k]) ||
+            (u0 && cioa_chunk_crc_cur(list[0][k]) != cioa_chunk_crc_cur(list[1][k]))) {
+            diff++;
+            fprintf(stderr, "  up_batch: entry %zu differs (%d/%d)\n", k, st[0][k], st[1][k]);
+        }
+        up += st[1][k] == CIO_OK;
+    }
+    TEST_CHECK(diff == 0);
+    TEST_CHECK(up == 13);
+    TEST_CHECK(cioa_total_chunks_up(ca[0]) == cioa_total_chunks_up(ca[1]) && cioa_total_chunks_up(ca[1]) == 8);
+    TEST_CHECK(cioa_total_chunks_up(cb[0]) == cioa_total_chunks_up(cb[1]) && cioa_total_chunks_up(cb[1]) == 5);
+    TEST_CHECK(cioa_last_chunk_error(ca[0]) == cioa_last_chunk_error(ca[1]));
+    TEST_CHECK(cioa_last_chunk_error(cb[0]) == cioa_last_chunk_error(cb[1]));
+    TEST_CHECK(cioa_chunk_up_batch(NULL, 0, NULL) == CIO_OK);
+    for (int r = 0; r < 2; r++) {
+        cioa_destroy(ca[r]);
+        cioa_destroy(cb[r]);
+    }
+}
+
 struct test {
     const char *name;
     void (*fn)(void);
@@ -920,6 +1022,7 @@ static const struct test tests[] = {
     {"perf_driver", test_perf_driver},
     {"sync_batch_async", test_sync_batch_async},
     {"scan_streams", test_scan_streams},
+    {"up_batch", test_up_batch},
     {NULL, NULL},
 };
 

@@ -32,7 +32,7 @@ INC="-Iinclude -Ichunkio_amd/csrc"
 case "$MODE" in
 build)
     mkdir -p $OBJ $LIBD $BIN
-    for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch; do
+    for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch cio_sha1; do
         $CL -O2 -g -fPIC -Wall -std=gnu11 $SAN $INC -c -o $OBJ/$f.o chunkio_amd/csrc/$f.c
     done
     for f in crc32_gpu host_pipeline sha1_gpu; do
@@ -41,11 +41,11 @@ build)
             $HSAN -c -o $OBJ/$f.o chunkio_amd/csrc/$f.hip
     done
     $HIPCC -shared -fPIC --offload-arch=gfx950 -o $LIBD/libchunkio_amd.so $OBJ/*.o -lpthread
-    for t in test_chunk_api test_crc32_dropin test_multi; do
+    for t in test_chunk_api test_crc32_dropin test_multi test_sha1; do
         $CL -O1 -g -Wall -std=gnu11 $SAN -Iinclude -o $BIN/$t tests/c/$t.c \
             -L$LIBD -lchunkio_amd -Wl,-rpath,'$ORIGIN/../../../../chunkio_amd/lib/asan' -lpthread
     done
-    echo "built $LIBD/libchunkio_amd.so, $BIN/{test_chunk_api,test_crc32_dropin,test_multi}"
+    echo "built $LIBD/libchunkio_amd.so, $BIN/{test_chunk_api,test_crc32_dropin,test_multi,test_sha1}"
     ;;
 host|gpu)
     DATA=tests/golden/400kb.txt
@@ -54,6 +54,7 @@ host|gpu)
     export ASAN_OPTIONS=detect_leaks=1:abort_on_error=0:halt_on_error=1
     export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
     timeout -k 10 300 $BIN/test_crc32_dropin $DATA
+    timeout -k 10 300 $BIN/test_sha1 $DATA 0:0 3:1,63,64,65,1000 7:55,56,57,409000 > /dev/null
     if [ "$MODE" = host ]; then
         for th in 1 8; do
             for m in immediate deferred; do   # deferred compares with immediate's files
@@ -91,7 +92,7 @@ tsan|tsan-gpu)
     TB=tests/c/bin/tsan
     if [ "$MODE" = tsan ]; then
         mkdir -p $T $TL $TB
-        for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch; do
+        for f in host_copy crc32_host crc32_scalar cio_verify cio_sync cioa_chunk crc_route crc_cpu_batch cio_sha1; do
             $CL -O1 -g -fPIC -std=gnu11 -fsanitize=thread $INC -c -o $T/$f.o chunkio_amd/csrc/$f.c
         done
         for f in crc32_gpu host_pipeline sha1_gpu; do
