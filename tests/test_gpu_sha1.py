@@ -418,3 +418,31 @@ def test_gpu_contexts_match_openssl_on_the_cfg5_batch(cuda):
         assert raw[i].tobytes() == _ossl_ctx(c, data=chunk[:cut]).raw, i
         fin = _ossl_ctx(c, state=raw[i].tobytes(), data=chunk[cut:])
         assert _ossl_final(c, fin) == hashlib.sha1(chunk).digest(), i
+
+
+def test_openssl_context_near_2_32_bits_continues_on_the_gpu(cuda):
+    """A context OpenSSL built from 512 MiB - 3 bytes (Nl just below 2^32)
+    continued on the GPU by 11 bytes: Nl wraps and Nh carries exactly as
+    OpenSSL's own SHA1_Update does, and the digest is the whole message's."""
+    import torch
+    c = _openssl()
+    rng = np.random.default_rng(84)
+    block = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+    ref = _ossl_ctx(c)
+    h = hashlib.sha1()
+    for _ in range(511):
+        c.SHA1_Update(ref, block, len(block))
+        h.update(block)
+    tail = block[:(1 << 20) - 3]
+    c.SHA1_Update(ref, tail, len(tail))
+    h.update(tail)
+    assert int.from_bytes(ref.raw[24:28], "little") == 0
+    more = bytes(range(11))
+    states = torch.from_numpy(np.frombuffer(ref.raw, np.uint8).copy()).to(cuda)
+    dev = torch.from_numpy(np.frombuffer(more, np.uint8).copy()).to(cuda)
+    cio.sha1_update_batch_dev(dev, _dev_i64([0], cuda), _dev_i64([len(more)], cuda), states)
+    c.SHA1_Update(ref, more, len(more))
+    h.update(more)
+    raw = cio.sha1_states_view(states)["raw"][0].tobytes()
+    assert raw == ref.raw and int.from_bytes(raw[24:28], "little") == 1
+    assert bytes(cio.sha1_final_batch_dev(states)[0]) == h.digest()
