@@ -1,6 +1,8 @@
 """the unmodified reference chunkio, built by its own CMake
 from a /tmp copy with cio-crc32 replaced by libchunkio_amd.so, passes its own
-ctest 5/5 under every host CRC path (tools/ref_dropin_ctest.sh).
+ctest 5/5 under every host CRC path (tools/ref_dropin_ctest.sh), with the
+reference's own src/cio_sha1.c added to its source list and compiled unmodified
+against include/sha1/sha1.h.
 
 Boundary evidence only (the oracle is oracle/_ref).  Needs the reference
 tree and cmake, so it runs in the build container and skips on the GPU box,
@@ -29,3 +31,8 @@ def test_reference_ctest_passes_against_the_shim(tmp_path):
     for t in ("cio-test-fs", "cio-test-metadata_update", "cio"):
         assert f"{t}" in out and "NOT LINKED" not in out
     assert "U crc_update" in out
+    # the reference's cio_sha1.c, built by its CMake against include/sha1/sha1.h,
+    # takes SHA1_* from the shim and hashes like OpenSSL
+    assert "U cioa_SHA1_Init" in out and "T cio_sha1_hash" in out
+    assert "(hashlib a4a6313b9c8270616b062beacd02d8cca8e6619c)" in out
+    assert "cio_sha1_hash(400kb.txt) = a4a6313b9c8270616b062beacd02d8cca8e6619c" in out

@@ -9,8 +9,10 @@
 # compiled by gcc), never this build.  Nothing under /root/reference is
 # written; the copy and both build trees live under $WORK.
 #
-# The only edits to the copy (both reported in the log as a diff):
+# The only edits to the copy (all reported in the log as a diff):
 #   src/CMakeLists.txt:16   set(libs cio-crc32) -> set(libs <repo>/chunkio_amd/lib/libchunkio_amd.so)
+#   src/CMakeLists.txt:13   cio_sha1.c added to the source list (the reference leaves it out;
+#                           it compiles unmodified against include/sha1/sha1.h)
 #   CMakeLists.txt          include_directories(BEFORE <repo>/include) ahead of deps/,
 #                           so <crc32/crc32.h> resolves to include/crc32/crc32.h
 #
@@ -65,6 +67,10 @@ check5 "$out"
 copy_ref "$WORK/shim"
 sed -i "16s|^set(libs cio-crc32)\$|set(libs $SHIM)|" "$WORK/shim/src/CMakeLists.txt"
 grep -q "^set(libs $SHIM)\$" "$WORK/shim/src/CMakeLists.txt" || { echo "src/CMakeLists.txt:16 not as expected"; exit 1; }
+# the SHA-1 wrapper, which the reference's CMake leaves out: compiled unmodified
+# against include/sha1/sha1.h (round 6), into the same library
+sed -i "13s|^  chunkio.c\$|  chunkio.c\n  cio_sha1.c|" "$WORK/shim/src/CMakeLists.txt"
+grep -q "^  cio_sha1.c\$" "$WORK/shim/src/CMakeLists.txt" || { echo "src/CMakeLists.txt:13 not as expected"; exit 1; }
 awk -v inc="$REPO/include" '
     /^include_directories\($/ && !done { print "include_directories(BEFORE " inc ")"; done = 1 }
     { print }' "$WORK/shim/CMakeLists.txt" >"$WORK/shim/CMakeLists.txt.new"
@@ -91,6 +97,20 @@ if grep -rl "libcio-crc32.a" "$B" --include=link.txt --include=*.make --include=
 fi
 grep -h -o "$REPO/include/crc32/crc32.h" "$B"/src/CMakeFiles/chunkio-static.dir/*.d 2>/dev/null | sort -u |
     sed 's/^/header seen by src\/: /' || true
+
+# cio_sha1.c from the reference's own source list: defined in chunkio's static
+# library, its SHA1_* calls resolved by the shim (cioa_SHA1_*); a C caller of
+# the reference's cio_sha1.h linked against both gets OpenSSL's digest
+echo "== cio_sha1 (src/cio_sha1.c compiled by the reference's CMake against include/sha1/sha1.h)"
+nm "$B"/src/libchunkio-static.a | grep -E ' [TU] (cio_sha1_hash|cioa_SHA1_Init)$' | sort -u
+nm "$B"/src/libchunkio-static.a | grep -q ' T cio_sha1_hash$' || { echo "cio_sha1.c not in chunkio"; exit 1; }
+nm "$B"/src/libchunkio-static.a | grep -q ' U cioa_SHA1_Init$' || { echo "SHA1_Init not taken from the shim"; exit 1; }
+cc -O2 -std=gnu11 -DCIOA_REF_BOUNDARY -I"$REPO/include" -I"$REF/include" -o "$WORK/test_sha1_cmake" \
+    "$REPO/tests/c/test_sha1.c" "$B"/src/libchunkio-static.a "$SHIM" -Wl,-rpath,"$(dirname "$SHIM")"
+got=$("$WORK/test_sha1_cmake" "$REPO/tests/golden/400kb.txt" 0:409600 | awk '/^hash /{print $2}')
+want=$(python3 -c "import hashlib,sys; print(hashlib.sha1(open(sys.argv[1],'rb').read()).hexdigest())" "$REPO/tests/golden/400kb.txt")
+echo "cio_sha1_hash(400kb.txt) = $got (hashlib $want)"
+[ "$got" = "$want" ] || { echo "cio_sha1 digest differs"; exit 1; }
 
 for mode in table clmul auto; do
     echo "== shim build: ctest, CIOA_HOST_CRC=$mode"
