@@ -235,3 +235,32 @@ def test_scan_streams_batches_across_streams(route, tmp_path, delete):
     assert views[1][2] == 0
     assert batches[1] < batches[0], batches
     assert batches[1] <= 3, batches
+
+
+def test_up_batch_when_the_verify_cannot_run(tmp_path):
+    """The verify batch itself failing (the GPU route forced with
+    cio_crc32_set_cpu_max(0) and a device ordinal that does not exist): every
+    chunk the round mapped comes back CIO_ERROR and down, its descriptor left
+    open as cio_file_up leaves it after mmap_file's CIO_ERROR (so a later up
+    is refused), nothing counts as up -- the same as one-by-one ups -- and
+    the reason is in cio_gpu_last_error()."""
+    import chunkio_amd as cio
+    outs = []
+    for tag in ("seq", "bat"):
+        root = str(tmp_path / tag)
+        make_stream(root, "s", 6, {2: "crc"})
+        with cf.Context(root, cf.CIO_CHECKSUM, max_chunks_up=64) as ctx:
+            chunks = _down_everything(ctx, "s")
+            ctx._lib.cioa_set_devices(ctx._h, (ctypes.c_int * 1)(4095), 1)
+            try:
+                cio.route(reset=True, cpu_max=0)
+                rets = [c.up() for c in chunks] if tag == "seq" else cf.up_batch(chunks)
+                again = [c.up() for c in chunks]
+                msg = _lib.lib().cio_gpu_last_error().decode()
+            finally:
+                cio.route(reset=True)
+            outs.append((rets, [outcome(c, r) for c, r in zip(chunks, rets)], again, ctx.total_chunks_up))
+            assert msg
+    assert outs[0] == outs[1]
+    rets, _, again, up = outs[1]
+    assert rets == [cf.CIO_ERROR] * len(rets) and again == [cf.CIO_ERROR] * len(rets) and up == 0
