@@ -21,6 +21,12 @@
  * status is CIO_OK or CIO_CORRUPTED (chunkio.h:50-53); error is one of the
  * CIO_ERR_* codes (cio_error.h:29-32) or 0.  On success crc_raw is the
  * un-finalized CRC the reference keeps in cf->crc_cur for later appends.
+ *
+ * It is also the file-level half of a batched cio_chunk_up (cio_file_up,
+ * cio_file.c:816-883, over many down chunks): map the chunks within the
+ * max_chunks_up budget, verify them in one call, count the ones that passed,
+ * and go on with the slots the failures freed -- INTEGRATION.md's sketch, and
+ * what cioa_chunk_up_batch (cioa_chunk.h) does in this repo's chunk layer.
  */
 #ifndef CIO_VERIFY_H
 #define CIO_VERIFY_H
