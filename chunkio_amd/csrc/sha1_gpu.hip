@@ -168,11 +168,6 @@ __device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&r
     st.h0 += a; st.h1 += b; st.h2 += c; st.h3 += d; st.h4 += e;
 }
 
-__device__ __forceinline__ void sha1_block_rounds(Sha1State &st, const uint4 (&rows)[20])
-{
-    sha1_block_rounds<0>(st, rows, [] {});
-}
-
 // One workgroup = one round wave + kShaSched schedule waves for the same
 // kShaChains (32) chunks, each wave alone on its SIMD.
 //  - A schedule wave's 64 lanes are 64 / kShaChains block streams of those
