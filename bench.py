@@ -814,6 +814,22 @@ def sha1_cpu_baseline(host, offs, lens, gpu_digests, world=1):
                                          "(hashlib releases the GIL while hashing)",
                                "threads_rule": f"per-GPU CPU share at N={world}: min(16, OMP_NUM_THREADS, "
                                                f"affinity_cpus // N)"}
+    # the library's own host SHA-1 (cio_sha1_hash: the CPU's SHA extensions),
+    # the host half of the SHA-1 boundary, over the same batch on 1 thread
+    import chunkio_amd as cio
+    cio.sha1_hash(views[0])                          # warm (library, dispatch)
+    t0 = time.perf_counter()
+    lreps = 0
+    while True:
+        lib_one = [cio.sha1_hash(v) for v in views]
+        lreps += 1
+        if time.perf_counter() - t0 >= 1.0:
+            break
+    secs = time.perf_counter() - t0
+    res["library_host_path"] = {"value": round(nbytes * lreps / secs / 1e9, 4), "unit": "GB/s", "threads": 1,
+                                "bit_exact_vs_gpu": lib_one == want,
+                                "sample": f"same batch x {lreps} passes, cio_sha1_hash per chunk (host SHA-1 "
+                                          "of include/sha1/sha1.h, SHA_CTX bytes equal OpenSSL's)"}
     if world > 1:
         res["shard"] = f"rank 0's shard of the {world}-GPU job (the per-GPU batch)"
     return res
