@@ -17,6 +17,9 @@
  * OpenSSL's libcrypto (e.g. Python's hashlib) never has two definitions of
  * SHA1_Init.  The context bytes are OpenSSL's exactly: a context can move
  * between OpenSSL, this host SHA-1 and the GPU batch calls at any split.
+ * It stands in for OpenSSL's <openssl/sha.h>, so one translation unit
+ * includes one of the two (both define SHA_CTX); other files of the same
+ * program may use OpenSSL's freely.
  */
 #ifndef CIOA_SHA1_SHA1_H
 #define CIOA_SHA1_SHA1_H
