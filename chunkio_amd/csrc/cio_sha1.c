@@ -15,9 +15,9 @@
  *     final chaining value and Nl/Nh in the context and zeroes data[] and num.
  *
  * Blocks run on the CPU's SHA extensions (SHA1RNDS4 / SHA1NEXTE / SHA1MSG1 /
- * SHA1MSG2) when it has them -- Zen and recent Intel cores do; 1.3 GB/s on
- * one core of this container's CPU, OpenSSL's rate there -- else on a
- * portable FIPS 180-4 loop.  CIOA_HOST_SHA1=portable pins
+ * SHA1MSG2) when it has them -- Zen and recent Intel cores do; 2.57 GB/s on
+ * one core of the MI355X box's EPYC 9575F, OpenSSL's rate there (bench.py's
+ * SHA-1 leg, library_host_path) -- else on a portable FIPS 180-4 loop.  CIOA_HOST_SHA1=portable pins
  * the portable loop (tests run both).
  */
 #define _GNU_SOURCE
