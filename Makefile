@@ -89,8 +89,22 @@ asm: $(SRC)/crc32_gpu.hip
 	@mkdir -p $(BLD)/asm
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(BLD)/asm/crc32_gpu.s $<
 
+# make install PREFIX=/usr/local: the library, the public headers (crc32/crc32.h,
+# sha1/sha1.h, chunkio_amd/*.h) and a pkg-config file, for a chunkio build to
+# link against.
+PREFIX ?= /usr/local
+install: $(LIB)
+	install -d $(DESTDIR)$(PREFIX)/lib/pkgconfig $(DESTDIR)$(PREFIX)/include/crc32 \
+	    $(DESTDIR)$(PREFIX)/include/sha1 $(DESTDIR)$(PREFIX)/include/chunkio_amd
+	install -m 755 $(LIB) $(DESTDIR)$(PREFIX)/lib/
+	install -m 644 include/crc32/crc32.h $(DESTDIR)$(PREFIX)/include/crc32/
+	install -m 644 include/sha1/sha1.h $(DESTDIR)$(PREFIX)/include/sha1/
+	install -m 644 include/chunkio_amd/*.h $(DESTDIR)$(PREFIX)/include/chunkio_amd/
+	printf 'prefix=%s\nlibdir=$${prefix}/lib\nincludedir=$${prefix}/include\n\nName: chunkio_amd\nDescription: MI355X-native CRC-32 / SHA-1 path of fluent/chunkio (drop-in crc32.h, batched GPU calls)\nVersion: 0.5.0\nLibs: -L$${libdir} -lchunkio_amd\nCflags: -I$${includedir}\n' \
+	    "$(PREFIX)" > $(DESTDIR)$(PREFIX)/lib/pkgconfig/chunkio_amd.pc
+
 clean:
 	rm -rf $(BLD) $(LIB) $(CTEST)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean ctests ablib ablib_sha1
+.PHONY: all oracle asm clean ctests ablib ablib_sha1 install

@@ -89,3 +89,30 @@ def test_multi_device_host_batches_from_c(cuda, tmp_path):
     rc, out = _run([_bin("test_multi"), str(tmp_path)], timeout=300)
     print(out)
     assert rc == 0 and "0 failed" in out, out
+
+
+def test_make_install_and_link_from_the_prefix(tmp_path):
+    """`make install PREFIX=...` lays out the library, the public headers and a
+    pkg-config file; a C program built only against that prefix gets the
+    reference's check value from crc_update and FIPS 180-4's "abc" digest from
+    cio_sha1_hash."""
+    prefix = tmp_path / "prefix"
+    rc, out = _run(["make", "-s", "-C", ROOT, "install", f"PREFIX={prefix}"])
+    assert rc == 0, out
+    pc = (prefix / "lib" / "pkgconfig" / "chunkio_amd.pc").read_text()
+    assert "-lchunkio_amd" in pc and f"prefix={prefix}" in pc
+    for h in ("crc32/crc32.h", "sha1/sha1.h", "chunkio_amd/cio_sha1.h", "chunkio_amd/cio_sha1_state.h",
+              "chunkio_amd/cio_crc32_gpu.h", "chunkio_amd/cioa_chunk.h"):
+        assert (prefix / "include" / h).exists(), h
+    src = tmp_path / "t.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <string.h>\n#include <crc32/crc32.h>\n#include <chunkio_amd/cio_sha1.h>\n'
+        'int main(void) { crc_t c = crc_finalize(crc_update(crc_init(), "123456789", 9));\n'
+        '  unsigned char md[20]; char hex[41]; cio_sha1_hash("abc", 3, md, NULL); cio_sha1_to_hex(md, hex);\n'
+        '  printf("%08lx %s\\n", (unsigned long) c, hex); return 0; }\n')
+    exe = tmp_path / "t"
+    rc, out = _run(["gcc", "-o", str(exe), str(src), f"-I{prefix}/include", f"-L{prefix}/lib", "-lchunkio_amd",
+                    f"-Wl,-rpath,{prefix}/lib"])
+    assert rc == 0, out
+    rc, out = _run([str(exe)])
+    assert rc == 0 and out.strip() == "cbf43926 a9993e364706816aba3e25717850c26c9cd0d89d", out
