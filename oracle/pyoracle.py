@@ -5,7 +5,9 @@
   _ref/libcrc32_ref.so   the reference's own deps/crc32/crc32.c compiled from
                          /root/reference by oracle/Makefile (kind "reference");
                          prebuilt here, it travels to the GPU box with the repo.
-SHA-1 oracle: hashlib (OpenSSL), FIPS 180-4 known answers in the tests.
+SHA-1 oracle: hashlib (OpenSSL), FIPS 180-4 known answers in the tests, OpenSSL's
+libcrypto for context bytes, and oracle/sha1_ctx.py (pure-Python SHA_CTX
+restatement pinned to libcrypto) where libcrypto is not loadable.
 """
 import ctypes
 import os

@@ -446,3 +446,30 @@ def test_openssl_context_near_2_32_bits_continues_on_the_gpu(cuda):
     raw = cio.sha1_states_view(states)["raw"][0].tobytes()
     assert raw == ref.raw and int.from_bytes(raw[24:28], "little") == 1
     assert bytes(cio.sha1_final_batch_dev(states)[0]) == h.digest()
+
+
+def test_device_contexts_equal_the_context_oracle(cuda):
+    """Without OpenSSL in the loop: the device contexts after random splits
+    equal oracle/sha1_ctx.py's (pure-Python SHA_CTX restatement, pinned to
+    libcrypto by tests/test_sha1_host.py), and an oracle-made context
+    continued on the GPU finishes to hashlib's digest."""
+    import torch
+    from oracle.sha1_ctx import Sha1Ctx
+    rng = np.random.default_rng(85)
+    n = 96
+    lens = rng.integers(0, 3000, n).astype(np.uint64)
+    lens[:6] = [0, 55, 56, 63, 64, 65]
+    offs = wl.packed_offsets(lens, align=16)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    dev = torch.from_numpy(host).to(cuda)
+    cut = (lens // 3).astype(np.int64)
+    pre = [Sha1Ctx().update(host[int(o):int(o) + int(k)]) for o, k in zip(offs, cut)]
+    states = torch.from_numpy(np.frombuffer(b"".join(p.raw() for p in pre), np.uint8).copy()).to(cuda)
+    cio.sha1_update_batch_dev(dev, _dev_i64(offs.astype(np.int64) + cut, cuda),
+                              _dev_i64(lens.astype(np.int64) - cut, cuda), states)
+    raw = cio.sha1_states_view(states)["raw"]
+    got = cio.sha1_final_batch_dev(states)
+    for i in range(n):
+        whole = host[int(offs[i]):int(offs[i] + lens[i])].tobytes()
+        assert raw[i].tobytes() == Sha1Ctx().update(whole).raw(), i
+        assert bytes(got[i]) == hashlib.sha1(whole).digest(), i

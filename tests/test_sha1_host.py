@@ -245,3 +245,27 @@ def test_path_pins_need_the_diag_gate():
     best = run(base)
     assert run(dict(base, CIOA_HOST_SHA1="portable")) == best
     assert run(dict(base, CIOA_HOST_SHA1="portable", CIO_GPU_DIAG="1")) == "portable"
+
+
+def test_context_oracle_pinned_to_openssl():
+    """oracle/sha1_ctx.py (a pure-Python restatement of OpenSSL's SHA_CTX
+    evolution, test infrastructure) gives OpenSSL's context bytes after every
+    Init / Update / Final and hashlib's digests; the library agrees with both."""
+    from oracle.sha1_ctx import Sha1Ctx
+    c = _crypto()
+    rng, cases = _cases(66, 120)
+    for pieces in cases:
+        o, ref, lib = Sha1Ctx(), OsslCtx(c), cio.Sha1()
+        assert o.raw() == ref.state
+        msg = b""
+        for ln in pieces:
+            d = rng.integers(0, 256, min(ln, 5000), dtype=np.uint8).tobytes()
+            o.update(d)
+            ref.update(d)
+            lib.update(d)
+            msg += d
+            assert o.raw() == ref.state == lib.state, (pieces, len(msg))
+        md = o.final()
+        assert md == ref.final() == lib.final() == hashlib.sha1(msg).digest()
+        assert o.raw() == ref.state == lib.state
+        assert Sha1Ctx(ref.state).raw() == ref.state       # parse / serialise round trip
