@@ -1419,6 +1419,7 @@ def _multi_device_host(args, world, device):
                                 "register_ms_once": round(reg_ms, 2),
                                 "equals_staged": bool(np.array_equal(out_reg, out))},
         "bytes_per_device": per_dev, "numa_per_device": numa, "reps": reps,
+        "host_batch_page_nodes": [page_node(host.ctypes.data + host.size * q // 4) for q in range(4)],
         "check": {"golden_sha256_match_full_job": (hashlib.sha256(np.asarray(out, dtype="<u4").tobytes())
                                                    .hexdigest() == want) if want else None},
         "host_cpu_batch": host_cpu}
