@@ -473,3 +473,35 @@ def test_device_contexts_equal_the_context_oracle(cuda):
         whole = host[int(offs[i]):int(offs[i] + lens[i])].tobytes()
         assert raw[i].tobytes() == Sha1Ctx().update(whole).raw(), i
         assert bytes(got[i]) == hashlib.sha1(whole).digest(), i
+
+
+def test_device_contexts_against_openssl_fixtures(cuda):
+    """tests/golden/sha1_ctx_vectors.json (libcrypto's SHA_CTX bytes after
+    every piece, recorded by make_sha1_ctx.py): the same pieces fed through
+    cio_sha1_update_batch_dev, one launch per piece over all 15 messages at
+    once, leave exactly those bytes; the digests match too."""
+    import json
+    import os
+    import torch
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sha1_ctx_vectors.json")) as f:
+        g = json.load(f)
+    cases = g["cases"]
+    msgs = [wl.gen_chunk(g["seed"], c["id"], sum(c["pieces"])).tobytes() for c in cases]
+    from test_gpu_crc import pack, to_dev
+    buf, offs, _ = pack(msgs, misalign=[i % 16 for i in range(len(msgs))])
+    dev = to_dev(buf, cuda)
+    n = len(cases)
+    states = cio.sha1_states_init(n, cuda)
+    raw = cio.sha1_states_view(states)["raw"]
+    assert [raw[i].tobytes().hex() for i in range(n)] == [c["ctx_after_each"][0] for c in cases]
+    pos = np.zeros(n, np.int64)
+    for k in range(max(len(c["pieces"]) for c in cases)):
+        ln = np.array([c["pieces"][k] if k < len(c["pieces"]) else 0 for c in cases], np.int64)
+        cio.sha1_update_batch_dev(dev, _dev_i64(offs.astype(np.int64) + pos, cuda), _dev_i64(ln, cuda), states)
+        pos += ln
+        raw = cio.sha1_states_view(states)["raw"]
+        for i, c in enumerate(cases):
+            if k < len(c["pieces"]):
+                assert raw[i].tobytes().hex() == c["ctx_after_each"][k + 1], (c["id"], k)
+    got = cio.sha1_final_batch_dev(states)
+    assert [bytes(d).hex() for d in got] == [c["digest"] for c in cases]

@@ -269,3 +269,32 @@ def test_context_oracle_pinned_to_openssl():
         assert md == ref.final() == lib.final() == hashlib.sha1(msg).digest()
         assert o.raw() == ref.state == lib.state
         assert Sha1Ctx(ref.state).raw() == ref.state       # parse / serialise round trip
+
+
+def _ctx_vectors():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "sha1_ctx_vectors.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("engine", ["library", "oracle"])
+def test_context_bytes_against_openssl_fixtures(engine, host_path):
+    """tests/golden/sha1_ctx_vectors.json: the SHA_CTX bytes libcrypto left
+    after every piece and after Final (make_sha1_ctx.py), needing no OpenSSL
+    at test time: the library's host SHA-1 (both block paths) and the
+    context oracle reproduce every one."""
+    from chunkio_amd import workloads as wl
+    from oracle.sha1_ctx import Sha1Ctx
+    g = _ctx_vectors()
+    for case in g["cases"]:
+        msg = wl.gen_chunk(g["seed"], case["id"], sum(case["pieces"])).tobytes()
+        ctx = cio.Sha1() if engine == "library" else Sha1Ctx()
+        state = (lambda: ctx.state) if engine == "library" else ctx.raw
+        assert state().hex() == case["ctx_after_each"][0]
+        pos = 0
+        for k, ln in enumerate(case["pieces"]):
+            ctx.update(msg[pos:pos + ln])
+            pos += ln
+            assert state().hex() == case["ctx_after_each"][k + 1], (case["id"], k)
+        assert ctx.final().hex() == case["digest"]
+        assert state().hex() == case["ctx_after_final"]
