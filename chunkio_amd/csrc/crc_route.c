@@ -271,6 +271,22 @@ static void learn(double *p, double x, double model)
     __atomic_store(p, &v, __ATOMIC_RELAXED);
 }
 
+static void relax(double *p, double model)
+{
+    const double old = ld_rate(p);
+    if (old > 0 && old < model) {
+        double v = old + 0.1 * (model - old);
+        __atomic_store(p, &v, __ATOMIC_RELAXED);
+    }
+}
+
+/* Test hook (not in the public header): set the learned GPU rate of a kind
+ * (0 memory, 1 files), GB/s per device; 0 forgets it. */
+void cioa_debug_split_set_gpu_rate(int fd, double gbps)
+{
+    __atomic_store(&g_rg[fd ? 1 : 0], &gbps, __ATOMIC_RELAXED);
+}
+
 static double host_model(int t, int fd)
 {
     const double m = t * (fd ? kCpuThreadFdGBps : kCpuThreadGBps);
@@ -369,7 +385,13 @@ static size_t split_point(const size_t *lens, size_t n, int ndev_distinct, int f
     const double r_gpu = (ndev_distinct > 1 ? ndev_distinct : 1) * gpu_rate(fd) * 1e9;
     const double f = kGpuFixedUs * 1e-6;
     if (mode != 2 && !gpu_bound && r_host >= kMaxHostOverGpu * r_gpu) {
-        return 0;     /* the host alone (see kMaxHostOverGpu) */
+        /* The host alone (see kMaxHostOverGpu).  No split means no new GPU
+         * sample, so a GPU rate learned too low would keep the route off for
+         * good: each such decision moves the learned rate a tenth of the way
+         * back to the model, and the route tries a split again once it has
+         * recovered (the next split measures afresh). */
+        relax(&g_rg[fd], kGpuGBps);
+        return 0;
     }
     const double b_host = (f + total / r_gpu) / (1.0 / r_host + 1.0 / r_gpu);
     const double t_split = b_host / r_host;

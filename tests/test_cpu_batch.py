@@ -208,6 +208,41 @@ def test_split_point_sizing_model():
         cio.split_rates(forget=True)
 
 
+def test_split_route_recovers_from_a_low_learned_gpu_rate():
+    """a GPU rate learned too low kept a host-routed batch off the
+    split route for good (no split, so no new sample).  Each such decision now
+    moves the learned rate a tenth of the way back to the model (54.7 GB/s),
+    so the route tries a split again after a few batches; a rate at or above
+    the model is left alone."""
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.cioa_debug_split_point
+    f.restype = ctypes.c_size_t
+    f.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    setr = lib.cioa_debug_split_set_gpu_rate
+    setr.argtypes = [ctypes.c_int, ctypes.c_double]
+    if os.environ.get("CIOA_CPU_CRC_MAX") or os.environ.get("CIOA_SPLIT_ROUTE") or os.environ.get("CIOA_HOST_CRC_THREADS"):
+        pytest.skip("routing environment set by the caller")
+    lens = (ctypes.c_size_t * 200)(*([2048002] * 200))
+    try:
+        cio.route(reset=True, threads=4)                  # host-routed: 4 x 22 GB/s from files
+        cio.split_rates(forget=True)
+        setr(1, 10.0)                                     # learned far too low (cold first split)
+        assert cio.split_rates()["gpu_fd"] == pytest.approx(10.0)
+        seen = []
+        for _ in range(40):
+            f(lens, 200, 1, 1, 0)                         # host-routed, fd batch
+            seen.append(cio.split_rates()["gpu_fd"])
+        assert seen[0] == pytest.approx(10.0 + 0.1 * (54.7 - 10.0))
+        assert all(b >= a for a, b in zip(seen, seen[1:]))
+        assert 88.0 < 3 * seen[-1] <= 3 * 54.7           # recovered: the split is considered again
+        setr(1, 60.0)                                     # at or above the model: untouched
+        f(lens, 200, 1, 1, 0)
+        assert cio.split_rates()["gpu_fd"] == pytest.approx(60.0)
+    finally:
+        cio.route(reset=True)
+        cio.split_rates(forget=True)
+
+
 def test_library_unload_stops_the_host_crc_pool():
     """The host CRC pool's detached workers run the library's code: dlclose
     (and exit) tells them to leave first (crc_cpu_batch.c pool_stop), so a
