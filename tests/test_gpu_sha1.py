@@ -505,3 +505,56 @@ def test_device_contexts_against_openssl_fixtures(cuda):
                 assert raw[i].tobytes().hex() == c["ctx_after_each"][k + 1], (c["id"], k)
     got = cio.sha1_final_batch_dev(states)
     assert [bytes(d).hex() for d in got] == [c["digest"] for c in cases]
+
+
+def _geometry_check(n, seed, device="cuda"):
+    """Two SHA1_Update batches (a random cut per chunk) over n ragged chunks at
+    odd offsets, then SHA1_Final and the one-shot kernel: the number of mid
+    contexts that differ from the host SHA-1's (OpenSSL's bytes) plus digests
+    that differ from hashlib's."""
+    import torch
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 2500, n).astype(np.uint64)
+    offs = wl.packed_offsets(lens, align=1, start=5)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    dev = torch.from_numpy(host).to(device)
+    cut = (lens * rng.random(n)).astype(np.int64)
+    states = cio.sha1_states_init(n, device)
+    cio.sha1_update_batch_dev(dev, _dev_i64(offs, device), _dev_i64(cut, device), states)
+    mid = cio.sha1_states_view(states)["raw"]
+    cio.sha1_update_batch_dev(dev, _dev_i64(offs.astype(np.int64) + cut, device),
+                              _dev_i64(lens.astype(np.int64) - cut, device), states)
+    fin = cio.sha1_final_batch_dev(states)
+    one = cio.sha1_batch_dev(dev, offs, lens)
+    bad = 0
+    for i in range(n):
+        o, ln, c = int(offs[i]), int(lens[i]), int(cut[i])
+        bad += mid[i].tobytes() != cio.Sha1().update(host[o:o + c]).state
+        want = hashlib.sha1(host[o:o + ln].tobytes()).digest()
+        bad += (bytes(fin[i]) != want) + (bytes(one[i]) != want)
+    return bad
+
+
+@pytest.mark.parametrize("per_wg", ["8", "16", "32"])
+def test_every_geometry_continues_contexts(cuda, per_wg):
+    """Each workgroup geometry of the SHA-1 kernel (8, 16 or 32 chunks per
+    workgroup, forced with CIO_SHA1_CHUNKS_PER_WG under CIO_GPU_DIAG=1 in a
+    process of its own: the choice is read once) over 700 ragged chunks at
+    odd offsets: the mid-message contexts equal the host SHA-1's (OpenSSL's
+    bytes), the finished digests and the one-shot digests equal hashlib's."""
+    import os
+    import subprocess
+    import sys
+    tests = os.path.dirname(os.path.abspath(__file__))
+    code = (f"import sys; sys.path.insert(0, {os.path.dirname(tests)!r}); sys.path.insert(0, {tests!r}); "
+            "import test_gpu_sha1 as t; print('bad', t._geometry_check(700, 86))")
+    env = dict(os.environ, CIO_GPU_DIAG="1", CIO_SHA1_CHUNKS_PER_WG=per_wg)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "bad 0" in r.stdout, r.stdout
+
+
+def test_wide_geometry_continues_contexts_in_process(cuda):
+    """5000 chunks: more than 16 per CU, so the default 32-chunk geometry runs
+    the continuation; mid contexts, finals and one-shot digests as above."""
+    assert _geometry_check(5000, 87, cuda) == 0
