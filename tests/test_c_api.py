@@ -116,3 +116,20 @@ def test_make_install_and_link_from_the_prefix(tmp_path):
     assert rc == 0, out
     rc, out = _run([str(exe)])
     assert rc == 0 and out.strip() == "cbf43926 a9993e364706816aba3e25717850c26c9cd0d89d", out
+
+
+@pytest.mark.parametrize("lang", ["c", "c++"])
+def test_public_headers_compile_alone_and_together(tmp_path, lang):
+    """Every public header compiles on its own and all of them together, as C
+    (gnu11) and as C++ (c++17, extern "C" linkage): a caller can include any
+    subset in any order."""
+    import glob
+    hdrs = sorted(os.path.relpath(h, os.path.join(ROOT, "include"))
+                  for h in glob.glob(os.path.join(ROOT, "include", "*", "*.h")))
+    assert "sha1/sha1.h" in hdrs and "crc32/crc32.h" in hdrs
+    comp, std, ext = ("gcc", "-std=gnu11", "c") if lang == "c" else ("g++", "-std=c++17", "cpp")
+    for i, group in enumerate([[h] for h in hdrs] + [hdrs, hdrs[::-1]]):
+        src = tmp_path / f"t{i}.{ext}"
+        src.write_text("".join(f"#include <{h}>\n" for h in group) + "int main(void) { return 0; }\n")
+        rc, out = _run([comp, std, "-Wall", "-Wextra", "-Werror", "-fsyntax-only", f"-I{ROOT}/include", str(src)])
+        assert rc == 0, (group, out)
