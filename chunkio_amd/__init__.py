@@ -4,9 +4,12 @@ content-checksum path (and its SHA-1 content hash).
 Layers:
   include/crc32/crc32.h, include/chunkio_amd/*.h   C ABI (the drop-in boundary)
   chunkio_amd/csrc/*.hip, *.c                      HIP kernels for gfx950 + host C
-  chunkio_amd/crc32.py                             Python mirror of the CRC API
+  chunkio_amd/crc32.py                             Python mirror of the CRC and SHA-1 API
+                                                   (Sha1 / sha1_hash: chunkio's cio_sha1 on
+                                                   OpenSSL-layout SHA_CTX bytes)
   chunkio_amd/chunkfile.py                         binding of the C chunk layer
-                                                   (cioa_chunk.h: write/sync/verify/tx/scan)
+                                                   (cioa_chunk.h: write/sync/verify/tx/scan,
+                                                   up_batch)
 """
 from ._lib import LIB_PATH, CioGpuError, lib  # noqa: F401
 from .crc32 import (  # noqa: F401
